@@ -1,0 +1,190 @@
+"""ctypes binding of libft8hip.so (include/ft8hip.h) and the device/stream plumbing.
+
+The library is the product: every numeric stage of the receive path runs in its HIP kernels.  If
+the library or a ROCm GPU is missing, every entry point raises -- there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("FT8HIP_LIB", os.path.join(_HERE, "lib", "libft8hip.so"))
+
+FT8_F32, FT8_F64, FT8_C64, FT8_C128, FT8_I16 = 0, 1, 2, 3, 4
+FT8_OK, FT8_E_ARG, FT8_E_HIP, FT8_E_UNSUPPORTED, FT8_E_NOMEM, FT8_E_RANGE = 0, -1, -2, -3, -4, -5
+FT8_FLAG_TOPK = 1
+N_STAGES = 6
+STAGE_NAMES = ("stft", "score", "select", "llr_bp", "compact", "decode_batch")
+
+
+class Ft8Params(ctypes.Structure):
+    _fields_ = [("sample_rate", ctypes.c_int32), ("bins_per_tone", ctypes.c_int32),
+                ("steps_per_symbol", ctypes.c_int32), ("max_candidates", ctypes.c_int32),
+                ("max_iterations", ctypes.c_int32), ("min_score_f64", ctypes.c_int32),
+                ("min_score", ctypes.c_double), ("f_lo", ctypes.c_int32), ("f_hi", ctypes.c_int32),
+                ("t_lo", ctypes.c_int32), ("t_hi", ctypes.c_int32), ("flags", ctypes.c_int32),
+                ("reserved", ctypes.c_int32)]
+
+
+# ft8_result (40 bytes) as a NumPy structured dtype
+RESULT_DTYPE = np.dtype({
+    "names": ["score", "slot", "abs_time", "abs_freq", "crc_extracted", "crc_calculated",
+              "ldpc_errors", "cand_index", "payload", "ok", "pad"],
+    "formats": ["<f8", "<i4", "<i4", "<i4", "<u2", "<u2", "<i2", "<u2", ("u1", (10,)), "u1", "u1"],
+    "offsets": [0, 8, 12, 16, 20, 22, 24, 26, 28, 38, 39],
+    "itemsize": 40,
+})
+
+_lib = None
+_lock = threading.Lock()
+_tls = threading.local()
+
+
+class Ft8Error(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libft8hip.so (raises if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise Ft8Error(
+                f"libft8hip.so not found at {LIB_PATH}: build it with "
+                "`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback exists)")
+        L = ctypes.CDLL(LIB_PATH)
+        vp, i32, i64, dbl = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_double
+        P = ctypes.POINTER(Ft8Params)
+        sig = {
+            "ft8_create": ([ctypes.c_int, ctypes.POINTER(vp)], ctypes.c_int),
+            "ft8_destroy": ([vp], ctypes.c_int),
+            "ft8_last_error": ([vp], ctypes.c_char_p),
+            "ft8_abi_version": ([], ctypes.c_int),
+            "ft8_limits": ([vp, vp, vp], ctypes.c_int),
+            "ft8_geometry": ([i32, i32, i32, i64, vp, vp, vp, vp], ctypes.c_int),
+            "ft8_stft": ([vp, vp, ctypes.c_int, i64, i32, i64, P, vp, vp], ctypes.c_int),
+            "ft8_sync_select": ([vp, vp, ctypes.c_int, i32, i32, i32, P, vp, vp, vp, vp, vp], ctypes.c_int),
+            "ft8_llr": ([vp, vp, ctypes.c_int, i32, i32, i32, i32, vp, i32, ctypes.c_int, vp, vp], ctypes.c_int),
+            "ft8_normalize": ([vp, vp, i32, vp, vp], ctypes.c_int),
+            "ft8_bp": ([vp, vp, i32, i32, vp, vp, vp], ctypes.c_int),
+            "ft8_decode_batch": ([vp, vp, ctypes.c_int, i64, i32, i64, P, vp, vp, i32, vp], ctypes.c_int),
+            "ft8_select_warnings": ([vp, vp, i32, vp], ctypes.c_int),
+            "ft8_crc14": ([vp, vp, vp, i32, vp, vp], ctypes.c_int),
+            "ft8_ldpc_check": ([vp, vp, i32, vp, vp], ctypes.c_int),
+            "ft8_set_timing": ([vp, ctypes.c_int], ctypes.c_int),
+            "ft8_get_timing": ([vp, vp, vp, ctypes.c_int], ctypes.c_int),
+        }
+        for name, (args, res) in sig.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = res
+        _ = dbl
+        _lib = L
+    return _lib
+
+
+EXPORTED_SYMBOLS = (
+    "ft8_create", "ft8_destroy", "ft8_last_error", "ft8_abi_version", "ft8_limits", "ft8_geometry",
+    "ft8_stft", "ft8_sync_select", "ft8_llr", "ft8_normalize", "ft8_bp", "ft8_decode_batch", "ft8_select_warnings",
+    "ft8_crc14", "ft8_ldpc_check", "ft8_set_timing", "ft8_get_timing")
+
+
+def limits():
+    a, b, c = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+    lib().ft8_limits(ctypes.byref(a), ctypes.byref(b), ctypes.byref(c))
+    return {"max_candidates": a.value, "max_fft_real": b.value, "max_fft_complex": c.value}
+
+
+def geometry(sample_rate: int, bins_per_tone: int, steps_per_symbol: int, n_samples: int):
+    """(nperseg, hop, nfft, frames) of calculate_spectrogram (spectrogram_analyse.py:31-43)."""
+    v = [ctypes.c_int32() for _ in range(4)]
+    rc = lib().ft8_geometry(int(sample_rate), int(bins_per_tone), int(steps_per_symbol), int(n_samples),
+                            *[ctypes.byref(x) for x in v])
+    if rc != FT8_OK:
+        raise ValueError("invalid spectrogram geometry (nfft must be greater than or equal to nperseg, "
+                         "positive sample rate and oversampling factors)")
+    return tuple(x.value for x in v)
+
+
+def require_gpu():
+    import torch
+    if not torch.cuda.is_available():
+        raise Ft8Error("ft8_demodulator_amd runs on a ROCm GPU (MI355X / gfx950); none is visible. "
+                       "There is no CPU fallback.")
+    return torch
+
+
+class Context:
+    """One libft8hip context per (host thread, device)."""
+
+    def __init__(self, device: int):
+        h = ctypes.c_void_p()
+        rc = lib().ft8_create(int(device), ctypes.byref(h))
+        if rc != FT8_OK:
+            raise Ft8Error(f"ft8_create(device={device}) failed with code {rc}")
+        self.handle = h
+        self.device = int(device)
+
+    def check(self, rc: int, what: str):
+        if rc == FT8_OK:
+            return
+        msg = lib().ft8_last_error(self.handle).decode(errors="replace")
+        text = f"{what}: {msg}"
+        if rc in (FT8_E_ARG, FT8_E_RANGE):
+            raise ValueError(text)
+        if rc == FT8_E_UNSUPPORTED:
+            raise NotImplementedError(text)
+        if rc == FT8_E_NOMEM:
+            raise MemoryError(text)
+        raise Ft8Error(text)
+
+    def set_timing(self, on: bool):
+        lib().ft8_set_timing(self.handle, int(bool(on)))
+
+    def timing(self, reset: bool = False):
+        ms = (ctypes.c_double * N_STAGES)()
+        cnt = (ctypes.c_int64 * N_STAGES)()
+        self.check(lib().ft8_get_timing(self.handle, ms, cnt, int(reset)), "ft8_get_timing")
+        return {STAGE_NAMES[i]: (ms[i], cnt[i]) for i in range(N_STAGES)}
+
+    def __del__(self):
+        try:
+            if getattr(self, "handle", None) and _lib is not None:
+                _lib.ft8_destroy(self.handle)
+        except Exception:  # noqa: BLE001
+            pass
+
+
+def device_index(device=None) -> int:
+    torch = require_gpu()
+    if device is None:
+        return torch.cuda.current_device()
+    d = torch.device(device)
+    return d.index if d.index is not None else torch.cuda.current_device()
+
+
+def context(device=None) -> Context:
+    dev = device_index(device)
+    cache = getattr(_tls, "ctx", None)
+    if cache is None:
+        cache = _tls.ctx = {}
+    if dev not in cache:
+        cache[dev] = Context(dev)
+    return cache[dev]
+
+
+def stream_handle(device=None):
+    torch = require_gpu()
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def ptr(t) -> ctypes.c_void_p:
+    return ctypes.c_void_p(t.data_ptr())

@@ -1,0 +1,688 @@
+// capi.hip -- host side of libft8hip.so: context, STFT plans, scratch, launches, C-ABI.
+//
+// See include/ft8hip.h for the contract.  Everything below runs on the host; all numerical work is
+// in the kernels of stft.hip / sync.hip / bp.hip.  No path here computes a decode on the CPU.
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "ft8_internal.h"
+
+using namespace ft8;
+
+namespace {
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+};
+
+struct PlanEntry {
+  int nfft;
+  bool cplx;   // complex-input path (P = nfft) vs real-input half-length path (P = nfft/2)
+  bool f64;
+  FftPlan plan;
+  void* tw = nullptr;
+  void* post = nullptr;
+};
+
+struct WinEntry {
+  int L;
+  bool f64;
+  void* w = nullptr;
+  double scale;
+};
+
+struct TimedLaunch {
+  int stage;
+  hipEvent_t a, b;
+};
+
+}  // namespace
+
+struct ft8_ctx {
+  int device = 0;
+  std::string err;
+  std::vector<PlanEntry> plans;
+  std::vector<WinEntry> wins;
+  DevBuf wf, scores, cand, cand_score, cand_count, rec_idx, warn, res_all, work;
+  bool timing = false;
+  std::vector<TimedLaunch> pending;
+  std::vector<hipEvent_t> pool;
+  double ms[FT8_N_STAGES] = {0};
+  int64_t launches[FT8_N_STAGES] = {0};
+};
+
+namespace {
+
+int fail(ft8_ctx* c, int code, const std::string& msg) {
+  if (c) c->err = msg;
+  return code;
+}
+
+int hipfail(ft8_ctx* c, hipError_t e, const char* where) {
+  return fail(c, FT8_E_HIP, std::string(where) + ": " + hipGetErrorString(e));
+}
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+int ensure(ft8_ctx* c, DevBuf& b, size_t bytes) {
+  if (bytes == 0) bytes = 16;
+  if (b.cap >= bytes) return FT8_OK;
+  if (b.p) {
+    (void)hipFree(b.p);
+    b.p = nullptr;
+    b.cap = 0;
+  }
+  size_t want = bytes + bytes / 4;
+  hipError_t e = hipMalloc(&b.p, want);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(c, FT8_E_NOMEM, std::string("hipMalloc failed for ") + std::to_string(want) + " bytes");
+  }
+  b.cap = want;
+  return FT8_OK;
+}
+
+hipEvent_t get_event(ft8_ctx* c) {
+  if (!c->pool.empty()) {
+    hipEvent_t e = c->pool.back();
+    c->pool.pop_back();
+    return e;
+  }
+  hipEvent_t e;
+  (void)hipEventCreate(&e);
+  return e;
+}
+
+struct StageTimer {
+  ft8_ctx* c;
+  int stage;
+  hipStream_t s;
+  hipEvent_t a = nullptr;
+  StageTimer(ft8_ctx* c_, int st, hipStream_t s_) : c(c_), stage(st), s(s_) {
+    if (c->timing) {
+      a = get_event(c);
+      (void)hipEventRecord(a, s);
+    }
+  }
+  void done() {
+    if (c->timing && a) {
+      hipEvent_t b = get_event(c);
+      (void)hipEventRecord(b, s);
+      c->pending.push_back({stage, a, b});
+      a = nullptr;
+    }
+  }
+};
+
+// NumPy pairwise summation of a complex64 array with zero imaginary parts (real part returned),
+// CFLOAT_pairwise_sum with n counted in floats (loops_utils.h.src)
+float cfloat_pairwise_re(const float* re, long n_floats) {
+  if (n_floats < 8) {
+    float rr = -0.0f;
+    for (long i = 0; i < n_floats; i += 2) rr += re[i / 2];
+    return rr;
+  } else if (n_floats <= 128) {
+    float r[4];
+    for (int j = 0; j < 4; ++j) r[j] = re[j];
+    long i;
+    for (i = 8; i < n_floats - (n_floats % 8); i += 8)
+      for (int j = 0; j < 4; ++j) r[j] += re[i / 2 + j];
+    float rr = (r[0] + r[1]) + (r[2] + r[3]);
+    for (; i < n_floats; i += 2) rr += re[i / 2];
+    return rr;
+  } else {
+    long n2 = n_floats / 2;
+    n2 -= n2 % 8;
+    return cfloat_pairwise_re(re, n2) + cfloat_pairwise_re(re + n2 / 2, n_floats - n2);
+  }
+}
+
+double double_pairwise(const double* a, long n) {
+  if (n < 8) {
+    double r = -0.0;
+    for (long i = 0; i < n; ++i) r += a[i];
+    return r;
+  } else if (n <= 128) {
+    double r[8];
+    for (int j = 0; j < 8; ++j) r[j] = a[j];
+    long i;
+    for (i = 8; i < n - (n % 8); i += 8)
+      for (int j = 0; j < 8; ++j) r[j] += a[i + j];
+    double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    for (; i < n; ++i) res += a[i];
+    return res;
+  } else {
+    long n2 = n / 2;
+    n2 -= n2 % 8;
+    return double_pairwise(a, n2) + double_pairwise(a + n2, n - n2);
+  }
+}
+
+// periodic Hann window exactly as scipy.signal.get_window('hann', L) builds it:
+// general_cosine(L + 1, [0.5, 0.5]) truncated, fac = linspace(-pi, pi, L + 1)
+std::vector<double> hann(int L) {
+  std::vector<double> w(L);
+  const double start = -M_PI, stop = M_PI;
+  const double step = (stop - start) / (double)L;
+  for (int i = 0; i < L; ++i) {
+    const double fac = (double)i * step + start;
+    w[i] = (0.0 + 0.5 * 1.0) + 0.5 * std::cos(fac);
+  }
+  if (L == 1) w[0] = 1.0;
+  return w;
+}
+
+int get_window(ft8_ctx* c, int L, bool f64, WinEntry** out) {
+  for (auto& w : c->wins)
+    if (w.L == L && w.f64 == f64) { *out = &w; return FT8_OK; }
+  std::vector<double> w = hann(L);
+  WinEntry e;
+  e.L = L;
+  e.f64 = f64;
+  hipError_t he;
+  if (f64) {
+    double s = 0.0 + double_pairwise(w.data(), L);
+    e.scale = 1.0 / (s * s);
+    he = hipMalloc(&e.w, sizeof(double) * L);
+    if (he == hipSuccess) he = hipMemcpy(e.w, w.data(), sizeof(double) * L, hipMemcpyHostToDevice);
+  } else {
+    std::vector<float> w32(L);
+    for (int i = 0; i < L; ++i) w32[i] = (float)w[i];
+    float s = 0.0f + cfloat_pairwise_re(w32.data(), 2L * L);
+    float sq = s * s;
+    e.scale = (double)(1.0f / sq);
+    he = hipMalloc(&e.w, sizeof(float) * L);
+    if (he == hipSuccess) he = hipMemcpy(e.w, w32.data(), sizeof(float) * L, hipMemcpyHostToDevice);
+  }
+  if (he != hipSuccess) return hipfail(c, he, "window upload");
+  c->wins.push_back(e);
+  *out = &c->wins.back();
+  return FT8_OK;
+}
+
+bool factor(int P, FftPlan& pl) {
+  pl.nstages = 0;
+  int r = P;
+  auto take = [&](int f) {
+    while (r % f == 0 && pl.nstages < 16) {
+      pl.radix[pl.nstages++] = f;
+      r /= f;
+    }
+  };
+  take(8);
+  take(4);
+  take(2);
+  take(5);
+  take(3);
+  take(7);
+  return r == 1 && pl.nstages > 0;
+}
+
+int get_plan(ft8_ctx* c, int nfft, bool cplx, bool f64, FftPlan* out) {
+  for (auto& p : c->plans)
+    if (p.nfft == nfft && p.cplx == cplx && p.f64 == f64) { *out = p.plan; return FT8_OK; }
+  PlanEntry e;
+  e.nfft = nfft;
+  e.cplx = cplx;
+  e.f64 = f64;
+  const int P = cplx ? nfft : nfft / 2;
+  if (!cplx && (nfft % 2)) return fail(c, FT8_E_UNSUPPORTED, "odd nfft is not supported for real input");
+  if (P > (cplx ? kMaxFftComplex : kMaxFftReal / 2))
+    return fail(c, FT8_E_RANGE, "nfft " + std::to_string(nfft) + " exceeds the compiled FFT limit");
+  e.plan.P = P;
+  if (!factor(P, e.plan))
+    return fail(c, FT8_E_UNSUPPORTED, "FFT length " + std::to_string(P) + " has a prime factor other than 2,3,5,7");
+  // twiddles W_P^m and post-processing W_N^k (N = 2P), from long double angles
+  const size_t esz = f64 ? 16 : 8;
+  std::vector<unsigned char> tw(esz * P), post(esz * (P + 1));
+  for (int m = 0; m < P; ++m) {
+    const long double ang = -2.0L * M_PIl * (long double)m / (long double)P;
+    const double cr = (double)cosl(ang), ci = (double)sinl(ang);
+    if (f64) { double v[2] = {cr, ci}; memcpy(&tw[esz * m], v, 16); }
+    else { float v[2] = {(float)cr, (float)ci}; memcpy(&tw[esz * m], v, 8); }
+  }
+  for (int k = 0; k <= P; ++k) {
+    const long double ang = -2.0L * M_PIl * (long double)k / (long double)(2 * P);
+    const double cr = (double)cosl(ang), ci = (double)sinl(ang);
+    if (f64) { double v[2] = {cr, ci}; memcpy(&post[esz * k], v, 16); }
+    else { float v[2] = {(float)cr, (float)ci}; memcpy(&post[esz * k], v, 8); }
+  }
+  hipError_t he = hipMalloc(&e.tw, tw.size());
+  if (he == hipSuccess) he = hipMalloc(&e.post, post.size());
+  if (he == hipSuccess) he = hipMemcpy(e.tw, tw.data(), tw.size(), hipMemcpyHostToDevice);
+  if (he == hipSuccess) he = hipMemcpy(e.post, post.data(), post.size(), hipMemcpyHostToDevice);
+  if (he != hipSuccess) return hipfail(c, he, "fft plan upload");
+  e.plan.tw = e.tw;
+  e.plan.post = e.post;
+  c->plans.push_back(e);
+  *out = e.plan;
+  return FT8_OK;
+}
+
+struct Geo {
+  int nperseg, hop, noverlap, nfft, frames;
+};
+
+int geometry(int fs, int bpt, int sps, int64_t n, Geo* g, std::string* why) {
+  if (fs <= 0 || bpt <= 0 || sps <= 0) { *why = "sample_rate, bins_per_tone and steps_per_symbol must be positive"; return FT8_E_ARG; }
+  g->nperseg = (int)(0.16 * (double)fs);                 // spectrogram_analyse.py:32
+  g->noverlap = g->nperseg - g->nperseg / sps;           // :33
+  g->nfft = (int)((double)fs / 6.25 * (double)bpt);      // :34
+  if (g->noverlap >= g->nperseg) g->noverlap = g->nperseg - 1;  // :42-43
+  g->hop = g->nperseg - g->noverlap;
+  if (g->nperseg < 1) { *why = "nperseg must be a positive integer"; return FT8_E_ARG; }
+  if (g->nfft < g->nperseg) { *why = "nfft must be greater than or equal to nperseg."; return FT8_E_ARG; }
+  g->frames = (n < g->nperseg) ? 0 : (int)((n - g->noverlap) / g->hop);
+  return FT8_OK;
+}
+
+bool is_f64_dtype(int dt) { return dt == FT8_F64 || dt == FT8_C128; }
+bool is_cplx_dtype(int dt) { return dt == FT8_C64 || dt == FT8_C128; }
+
+int do_stft(ft8_ctx* c, const void* samples, int dtype, int64_t n_samples, int n_slots, int64_t slot_stride,
+            const ft8_params* p, void* d_wf, hipStream_t s) {
+  Geo g;
+  std::string why;
+  int rc = geometry(p->sample_rate, p->bins_per_tone, p->steps_per_symbol, n_samples, &g, &why);
+  if (rc) return fail(c, rc, why);
+  if (dtype < FT8_F32 || dtype > FT8_I16) return fail(c, FT8_E_ARG, "unknown sample dtype");
+  if (p->t_lo < 0 || p->t_hi > g.frames || p->t_lo > p->t_hi)
+    return fail(c, FT8_E_ARG, "frame range [t_lo, t_hi) outside [0, " + std::to_string(g.frames) + ")");
+  if (p->f_lo < 0 || p->f_hi > g.nfft || p->f_lo > p->f_hi)
+    return fail(c, FT8_E_ARG, "bin range [f_lo, f_hi) outside [0, nfft)");
+  if (p->t_hi == p->t_lo || p->f_hi == p->f_lo || n_slots == 0) return FT8_OK;
+  const bool f64 = is_f64_dtype(dtype), cplx = is_cplx_dtype(dtype);
+  StftLaunch L{};
+  rc = get_plan(c, g.nfft, cplx, f64, &L.plan);
+  if (rc) return rc;
+  WinEntry* w = nullptr;
+  rc = get_window(c, g.nperseg, f64, &w);
+  if (rc) return rc;
+  L.samples = samples;
+  L.dtype = dtype;
+  L.n_samples = n_samples;
+  L.slot_stride = slot_stride;
+  L.n_slots = n_slots;
+  L.nperseg = g.nperseg;
+  L.hop = g.hop;
+  L.nfft = g.nfft;
+  L.t_lo = p->t_lo;
+  L.t_hi = p->t_hi;
+  L.f_lo = p->f_lo;
+  L.f_hi = p->f_hi;
+  L.window = w->w;
+  L.scale = w->scale;
+  L.out = d_wf;
+  StageTimer tm(c, 0, s);
+  hipError_t e = launch_stft(L, s);
+  tm.done();
+  if (e != hipSuccess) return hipfail(c, e, "stft launch");
+  return FT8_OK;
+}
+
+struct Grid {
+  int t0, NT, NF;
+};
+Grid grid_of(int T, int F, int sps, int bpt) {
+  // ft8_find_candidates ranges (ft8_decode.py:108-109)
+  Grid g;
+  const int nb = T / sps;
+  g.t0 = -10 * sps;
+  const int t_end = nb * sps - sps * 59;
+  g.NT = t_end > g.t0 ? t_end - g.t0 : 0;
+  g.NF = F - 7 * bpt > 0 ? F - 7 * bpt : 0;
+  return g;
+}
+
+int do_sync_select(ft8_ctx* c, const void* d_wf, int wf_f64, int n_slots, int T, int F, const ft8_params* p,
+                   int32_t* cand, double* cand_score, int32_t* cand_count, void* d_scores, hipStream_t s) {
+  if (p->steps_per_symbol <= 0 || p->bins_per_tone <= 0) return fail(c, FT8_E_ARG, "bad oversampling factors");
+  if (p->flags & FT8_FLAG_TOPK) return fail(c, FT8_E_UNSUPPORTED, "FT8_FLAG_TOPK is not implemented yet");
+  const int N = p->max_candidates;
+  if (N > kMaxCandidates)
+    return fail(c, FT8_E_RANGE, "max_candidates > " + std::to_string(kMaxCandidates) + " is not supported");
+  Grid g = grid_of(T, F, p->steps_per_symbol, p->bins_per_tone);
+  if (N <= 0 || g.NT == 0 || g.NF == 0 || n_slots == 0) {
+    hipError_t e = hipMemsetAsync(cand_count, 0, sizeof(int32_t) * (size_t)(n_slots > 0 ? n_slots : 0), s);
+    return e == hipSuccess ? FT8_OK : hipfail(c, e, "memset");
+  }
+  const size_t esz = wf_f64 ? 8 : 4;
+  int rc;
+  void* scores = d_scores;
+  if (!scores) {
+    if ((rc = ensure(c, c->scores, esz * (size_t)n_slots * g.NT * g.NF))) return rc;
+    scores = c->scores.p;
+  }
+  if ((rc = ensure(c, c->rec_idx, sizeof(int32_t) * (size_t)n_slots * kMaxRecords))) return rc;
+  if ((rc = ensure(c, c->warn, sizeof(int32_t) * (size_t)n_slots))) return rc;
+  SyncLaunch L{};
+  L.wf = d_wf;
+  L.wf_f64 = wf_f64;
+  L.n_slots = n_slots;
+  L.T = T;
+  L.F = F;
+  L.sps = p->steps_per_symbol;
+  L.bpt = p->bins_per_tone;
+  L.t0 = g.t0;
+  L.NT = g.NT;
+  L.NF = g.NF;
+  L.scores = scores;
+  L.N = N;
+  L.min_score = p->min_score;
+  L.min_score_f64 = p->min_score_f64;
+  L.flags = p->flags;
+  L.cand = cand;
+  L.cand_score = cand_score;
+  L.cand_count = cand_count;
+  L.rec_idx = (int32_t*)c->rec_idx.p;
+  L.warn = (int32_t*)c->warn.p;
+  StageTimer t1(c, 1, s);
+  hipError_t e = launch_score(L, s);
+  t1.done();
+  if (e != hipSuccess) return hipfail(c, e, "score launch");
+  StageTimer t2(c, 2, s);
+  e = launch_select(L, s);
+  t2.done();
+  if (e != hipSuccess) return hipfail(c, e, "select launch");
+  return FT8_OK;
+}
+
+}  // namespace
+
+// ============================================================================================
+extern "C" {
+
+int ft8_abi_version(void) { return FT8HIP_ABI_VERSION; }
+
+int ft8_limits(int32_t* max_candidates, int32_t* max_fft_real, int32_t* max_fft_complex) {
+  if (max_candidates) *max_candidates = kMaxCandidates;
+  if (max_fft_real) *max_fft_real = kMaxFftReal;
+  if (max_fft_complex) *max_fft_complex = kMaxFftComplex;
+  return FT8_OK;
+}
+
+int ft8_create(int device, ft8_ctx** out) {
+  if (!out) return FT8_E_ARG;
+  *out = nullptr;
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess || n <= 0) return FT8_E_HIP;
+  if (device < 0 || device >= n) return FT8_E_ARG;
+  ft8_ctx* c = new (std::nothrow) ft8_ctx();
+  if (!c) return FT8_E_NOMEM;
+  c->device = device;
+  *out = c;
+  return FT8_OK;
+}
+
+int ft8_destroy(ft8_ctx* c) {
+  if (!c) return FT8_OK;
+  {
+    DeviceGuard dg(c->device);
+    for (auto* b : {&c->wf, &c->scores, &c->cand, &c->cand_score, &c->cand_count, &c->rec_idx, &c->warn,
+                    &c->res_all, &c->work})
+      if (b->p) (void)hipFree(b->p);
+    for (auto& p : c->plans) {
+      if (p.tw) (void)hipFree(p.tw);
+      if (p.post) (void)hipFree(p.post);
+    }
+    for (auto& w : c->wins)
+      if (w.w) (void)hipFree(w.w);
+    for (auto& t : c->pending) {
+      (void)hipEventDestroy(t.a);
+      (void)hipEventDestroy(t.b);
+    }
+    for (auto ev : c->pool) (void)hipEventDestroy(ev);
+  }
+  delete c;
+  return FT8_OK;
+}
+
+const char* ft8_last_error(const ft8_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int ft8_geometry(int32_t fs, int32_t bpt, int32_t sps, int64_t n, int32_t* nperseg, int32_t* hop, int32_t* nfft,
+                 int32_t* frames) {
+  Geo g;
+  std::string why;
+  int rc = geometry(fs, bpt, sps, n, &g, &why);
+  if (rc) return rc;
+  if (nperseg) *nperseg = g.nperseg;
+  if (hop) *hop = g.hop;
+  if (nfft) *nfft = g.nfft;
+  if (frames) *frames = g.frames;
+  return FT8_OK;
+}
+
+int ft8_stft(ft8_ctx* c, const void* d_samples, int dtype, int64_t n_samples, int32_t n_slots, int64_t slot_stride,
+             const ft8_params* p, void* d_wf, void* stream) {
+  if (!c || !p || (!d_samples && n_slots > 0) || (!d_wf && n_slots > 0)) return fail(c, FT8_E_ARG, "null argument");
+  DeviceGuard dg(c->device);
+  return do_stft(c, d_samples, dtype, n_samples, n_slots, slot_stride, p, d_wf, (hipStream_t)stream);
+}
+
+int ft8_sync_select(ft8_ctx* c, const void* d_wf, int wf_f64, int32_t n_slots, int32_t T, int32_t F,
+                    const ft8_params* p, int32_t* d_cand, double* d_cand_score, int32_t* d_cand_count,
+                    void* d_scores, void* stream) {
+  if (!c || !p || !d_cand_count) return fail(c, FT8_E_ARG, "null argument");
+  if (T < 0 || F < 0 || n_slots < 0) return fail(c, FT8_E_ARG, "negative size");
+  DeviceGuard dg(c->device);
+  return do_sync_select(c, d_wf, wf_f64, n_slots, T, F, p, d_cand, d_cand_score, d_cand_count, d_scores,
+                        (hipStream_t)stream);
+}
+
+int ft8_llr(ft8_ctx* c, const void* d_wf, int wf_f64, int32_t T, int32_t F, int32_t sps, int32_t bpt,
+            const int32_t* d_cand, int32_t n, int normalize, double* d_llr, void* stream) {
+  if (!c || !d_llr || (!d_cand && n > 0) || sps <= 0 || bpt <= 0) return fail(c, FT8_E_ARG, "bad argument");
+  if (n <= 0) return FT8_OK;
+  DeviceGuard dg(c->device);
+  int rc;
+  if ((rc = ensure(c, c->work, 16))) return rc;
+  BpLaunch L{};
+  L.wf = d_wf;
+  L.wf_f64 = wf_f64;
+  L.T = T;
+  L.F = F;
+  L.sps = sps;
+  L.bpt = bpt;
+  L.cand = d_cand;
+  L.n_items = n;
+  L.mode = 1;
+  L.normalize = normalize;
+  L.llr_only = 1;
+  L.llr_out = d_llr;
+  L.work = (unsigned*)c->work.p;
+  StageTimer tm(c, 3, (hipStream_t)stream);
+  hipError_t e = launch_bp(L, (hipStream_t)stream);
+  tm.done();
+  return e == hipSuccess ? FT8_OK : hipfail(c, e, "llr launch");
+}
+
+int ft8_normalize(ft8_ctx* c, const double* d_in, int32_t n, double* d_out, void* stream) {
+  if (!c || (n > 0 && (!d_in || !d_out))) return fail(c, FT8_E_ARG, "bad argument");
+  if (n <= 0) return FT8_OK;
+  DeviceGuard dg(c->device);
+  int rc;
+  if ((rc = ensure(c, c->work, 16))) return rc;
+  BpLaunch L{};
+  L.mode = 2;
+  L.llr_in = d_in;
+  L.n_items = n;
+  L.normalize = 1;
+  L.llr_only = 1;
+  L.llr_out = d_out;
+  L.work = (unsigned*)c->work.p;
+  StageTimer tm(c, 3, (hipStream_t)stream);
+  hipError_t e = launch_bp(L, (hipStream_t)stream);
+  tm.done();
+  return e == hipSuccess ? FT8_OK : hipfail(c, e, "normalize launch");
+}
+
+int ft8_bp(ft8_ctx* c, const double* d_llr, int32_t n, int32_t max_iterations, uint8_t* d_plain, ft8_result* d_res,
+           void* stream) {
+  if (!c || (!d_llr && n > 0)) return fail(c, FT8_E_ARG, "bad argument");
+  if (n <= 0) return FT8_OK;
+  DeviceGuard dg(c->device);
+  int rc;
+  if ((rc = ensure(c, c->work, 16))) return rc;
+  BpLaunch L{};
+  L.mode = 2;
+  L.llr_in = d_llr;
+  L.n_items = n;
+  L.normalize = 0;
+  L.max_iterations = max_iterations;
+  L.plain_out = d_plain;
+  L.res = d_res;
+  L.work = (unsigned*)c->work.p;
+  StageTimer tm(c, 3, (hipStream_t)stream);
+  hipError_t e = launch_bp(L, (hipStream_t)stream);
+  tm.done();
+  return e == hipSuccess ? FT8_OK : hipfail(c, e, "bp launch");
+}
+
+int ft8_decode_batch(ft8_ctx* c, const void* d_samples, int dtype, int64_t n_samples, int32_t n_slots,
+                     int64_t slot_stride, const ft8_params* p, ft8_result* d_out, int32_t* d_counts,
+                     int32_t cap, void* stream) {
+  if (!c || !p || !d_counts || (n_slots > 0 && !d_samples) || n_slots < 0 || cap < 0)
+    return fail(c, FT8_E_ARG, "bad argument");
+  if (cap > 0 && !d_out) return fail(c, FT8_E_ARG, "null output with positive capacity");
+  DeviceGuard dg(c->device);
+  hipStream_t s = (hipStream_t)stream;
+  if (n_slots == 0) return FT8_OK;
+  StageTimer whole(c, 5, s);
+  Geo g;
+  std::string why;
+  int rc = geometry(p->sample_rate, p->bins_per_tone, p->steps_per_symbol, n_samples, &g, &why);
+  if (rc) return fail(c, rc, why);
+  const int T = p->t_hi - p->t_lo, F = p->f_hi - p->f_lo;
+  const bool f64 = is_f64_dtype(dtype);
+  const size_t esz = f64 ? 8 : 4;
+  const int N = p->max_candidates;
+  Grid gr = grid_of(T > 0 ? T : 0, F > 0 ? F : 0, p->steps_per_symbol, p->bins_per_tone);
+  if (T <= 0 || F <= 0 || N <= 0 || gr.NT == 0 || gr.NF == 0) {
+    // nothing to search: validate the ranges, report zero decodes
+    if (p->t_lo < 0 || p->t_hi > g.frames || p->f_lo < 0 || p->f_hi > g.nfft)
+      return fail(c, FT8_E_ARG, "frame/bin range outside the spectrogram");
+    hipError_t e = hipMemsetAsync(d_counts, 0, sizeof(int32_t) * n_slots, s);
+    whole.done();
+    return e == hipSuccess ? FT8_OK : hipfail(c, e, "memset");
+  }
+  if (N > kMaxCandidates)
+    return fail(c, FT8_E_RANGE, "max_candidates > " + std::to_string(kMaxCandidates) + " is not supported");
+  if ((rc = ensure(c, c->wf, esz * (size_t)n_slots * T * F))) return rc;
+  if ((rc = ensure(c, c->cand, sizeof(int32_t) * 2 * (size_t)n_slots * N))) return rc;
+  if ((rc = ensure(c, c->cand_score, sizeof(double) * (size_t)n_slots * N))) return rc;
+  if ((rc = ensure(c, c->cand_count, sizeof(int32_t) * (size_t)n_slots))) return rc;
+  if ((rc = ensure(c, c->res_all, sizeof(ft8_result) * (size_t)n_slots * N))) return rc;
+  if ((rc = ensure(c, c->work, 16))) return rc;
+  if ((rc = do_stft(c, d_samples, dtype, n_samples, n_slots, slot_stride, p, c->wf.p, s))) return rc;
+  if ((rc = do_sync_select(c, c->wf.p, f64, n_slots, T, F, p, (int32_t*)c->cand.p, (double*)c->cand_score.p,
+                           (int32_t*)c->cand_count.p, nullptr, s)))
+    return rc;
+  BpLaunch B{};
+  B.wf = c->wf.p;
+  B.wf_f64 = f64;
+  B.T = T;
+  B.F = F;
+  B.sps = p->steps_per_symbol;
+  B.bpt = p->bins_per_tone;
+  B.cand = (const int32_t*)c->cand.p;
+  B.cand_score = (const double*)c->cand_score.p;
+  B.cand_count = (const int32_t*)c->cand_count.p;
+  B.N = N;
+  B.n_slots = n_slots;
+  B.n_items = n_slots * N;
+  B.mode = 0;
+  B.normalize = 1;
+  B.max_iterations = p->max_iterations;
+  B.res = (ft8_result*)c->res_all.p;
+  B.work = (unsigned*)c->work.p;
+  StageTimer t3(c, 3, s);
+  hipError_t e = launch_bp(B, s);
+  t3.done();
+  if (e != hipSuccess) return hipfail(c, e, "bp launch");
+  CompactLaunch C{};
+  C.res = (const ft8_result*)c->res_all.p;
+  C.cand_count = (const int32_t*)c->cand_count.p;
+  C.n_slots = n_slots;
+  C.N = N;
+  C.out = d_out;
+  C.counts = d_counts;
+  C.cap = cap;
+  StageTimer t4(c, 4, s);
+  e = launch_compact(C, s);
+  t4.done();
+  whole.done();
+  if (e != hipSuccess) return hipfail(c, e, "compact launch");
+  return FT8_OK;
+}
+
+int ft8_select_warnings(ft8_ctx* c, int32_t* d_out, int32_t n_slots, void* stream) {
+  if (!c || !d_out || n_slots < 0) return fail(c, FT8_E_ARG, "bad argument");
+  if (n_slots == 0) return FT8_OK;
+  if (!c->warn.p || c->warn.cap < sizeof(int32_t) * n_slots) return fail(c, FT8_E_ARG, "no selection has run");
+  DeviceGuard dg(c->device);
+  hipError_t e = hipMemcpyAsync(d_out, c->warn.p, sizeof(int32_t) * n_slots, hipMemcpyDeviceToDevice,
+                                (hipStream_t)stream);
+  return e == hipSuccess ? FT8_OK : hipfail(c, e, "copy warnings");
+}
+
+int ft8_crc14(ft8_ctx* c, const uint8_t* d_msg, const int32_t* d_nbits, int32_t n, uint16_t* d_crc, void* stream) {
+  if (!c || (n > 0 && (!d_msg || !d_nbits || !d_crc))) return fail(c, FT8_E_ARG, "bad argument");
+  DeviceGuard dg(c->device);
+  hipError_t e = launch_crc14(d_msg, d_nbits, n, d_crc, (hipStream_t)stream);
+  return e == hipSuccess ? FT8_OK : hipfail(c, e, "crc14 launch");
+}
+
+int ft8_ldpc_check(ft8_ctx* c, const uint8_t* d_bits, int32_t n, int32_t* d_errors, void* stream) {
+  if (!c || (n > 0 && (!d_bits || !d_errors))) return fail(c, FT8_E_ARG, "bad argument");
+  DeviceGuard dg(c->device);
+  hipError_t e = launch_ldpc_check(d_bits, n, d_errors, (hipStream_t)stream);
+  return e == hipSuccess ? FT8_OK : hipfail(c, e, "ldpc_check launch");
+}
+
+int ft8_set_timing(ft8_ctx* c, int enable) {
+  if (!c) return FT8_E_ARG;
+  c->timing = enable != 0;
+  return FT8_OK;
+}
+
+int ft8_get_timing(ft8_ctx* c, double* ms, int64_t* launches, int reset) {
+  if (!c) return FT8_E_ARG;
+  DeviceGuard dg(c->device);
+  for (auto& t : c->pending) {
+    hipError_t e = hipEventSynchronize(t.b);
+    if (e != hipSuccess) return hipfail(c, e, "event sync");
+    float v = 0.f;
+    (void)hipEventElapsedTime(&v, t.a, t.b);
+    c->ms[t.stage] += v;
+    c->launches[t.stage] += 1;
+    c->pool.push_back(t.a);
+    c->pool.push_back(t.b);
+  }
+  c->pending.clear();
+  for (int i = 0; i < FT8_N_STAGES; ++i) {
+    if (ms) ms[i] = c->ms[i];
+    if (launches) launches[i] = c->launches[i];
+    if (reset) {
+      c->ms[i] = 0;
+      c->launches[i] = 0;
+    }
+  }
+  return FT8_OK;
+}
+
+}  // extern "C"

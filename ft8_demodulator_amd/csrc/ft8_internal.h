@@ -1,0 +1,111 @@
+// ft8_internal.h -- shared device helpers and the internal launch interface between the
+// kernel translation units (stft.hip, sync.hip, bp.hip) and the C-ABI (capi.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/ft8hip.h"
+#include "ft8_ldpc_tables.h"
+
+namespace ft8 {
+
+constexpr int kWave = 64;
+constexpr int kMaxCandidates = 4096;   // LDS-resident selection (k_select)
+constexpr int kMaxFftReal = 16384;     // nfft of the real-input path (half-length FFT <= 8192)
+constexpr int kMaxFftComplex = 8192;   // nfft of the complex-input path
+constexpr int kMaxRecords = 2048;      // new-maximum records kept per slot for the exact heap replay
+
+__host__ __device__ inline int floordiv(int a, int b) {
+  int q = a / b;
+  if ((a % b) != 0 && ((a < 0) != (b < 0))) q--;
+  return q;
+}
+
+template <typename T>
+struct cplx {
+  T x, y;
+};
+
+// ---- STFT plan (host-built tables, device-resident) ----------------------------------------
+struct FftPlan {
+  int P;              // transform length (nfft/2 for real input, nfft for complex input)
+  int nstages;
+  int radix[16];
+  const void* tw;     // W_P^m, m in [0, P): cplx<float> or cplx<double>
+  const void* post;   // real path: W_N^k, k in [0, P]  (N = 2P)
+};
+
+struct StftLaunch {
+  const void* samples;
+  int dtype;               // ft8_dtype
+  int64_t n_samples, slot_stride;
+  int n_slots;
+  int nperseg, hop, nfft;
+  int t_lo, t_hi, f_lo, f_hi;
+  const void* window;      // float or double [nperseg]
+  double scale;            // 1 / (sum w)^2
+  void* out;               // float or double [n_slots][t_hi-t_lo][f_hi-f_lo]
+  FftPlan plan;
+};
+hipError_t launch_stft(const StftLaunch& a, hipStream_t s);
+
+// ---- sync score + selection ----------------------------------------------------------------
+struct SyncLaunch {
+  const void* wf;          // [n_slots][T][F]
+  int wf_f64;
+  int n_slots, T, F;
+  int sps, bpt;
+  int t0, NT, NF;          // abs_time grid = [t0, t0+NT), abs_freq grid = [0, NF)
+  void* scores;            // [n_slots][NT][NF] in wf dtype
+  int N;                   // max candidates
+  double min_score;
+  int min_score_f64;
+  int flags;
+  int32_t* cand;           // [n_slots][N][2]
+  double* cand_score;      // [n_slots][N]
+  int32_t* cand_count;     // [n_slots]
+  int32_t* rec_idx;        // scratch [n_slots][kMaxRecords]
+  int32_t* warn;           // scratch [n_slots] (bit 0: tie reached a heap comparison,
+                           //                    bit 1: record overflow -> approximate tie order)
+};
+hipError_t launch_score(const SyncLaunch& a, hipStream_t s);
+hipError_t launch_select(const SyncLaunch& a, hipStream_t s);
+
+// ---- LLR + BP + CRC ------------------------------------------------------------------------
+struct BpLaunch {
+  // LLR source: either a waterfall + candidate list, or precomputed LLRs
+  const void* wf;          // [n_slots][T][F] or null
+  int wf_f64, T, F, sps, bpt;
+  const int32_t* cand;     // mode A: [n_slots][N][2] + cand_count; mode B: [n][3] (slot, t, f)
+  const double* cand_score;
+  const int32_t* cand_count;
+  int N;                   // per-slot capacity (mode A)
+  int n_slots;
+  int n_items;             // mode B item count, or n_slots*N in mode A
+  int mode;                // 0: waterfall+per-slot candidates, 1: waterfall+explicit list,
+                           // 2: LLR input
+  const double* llr_in;    // mode 2
+  int normalize;           // llr stage only
+  int max_iterations;
+  int llr_only;            // 1: stop after the LLR stage
+  double* llr_out;         // nullable [n_items][174]
+  uint8_t* plain_out;      // nullable [n_items][174]
+  ft8_result* res;         // nullable [n_items]
+  unsigned* work;          // work counter (zeroed by the launcher)
+};
+hipError_t launch_bp(const BpLaunch& a, hipStream_t s);
+
+struct CompactLaunch {
+  const ft8_result* res;   // [n_slots][N]
+  const int32_t* cand_count;
+  int n_slots, N;
+  ft8_result* out;         // [n_slots][cap]
+  int32_t* counts;
+  int cap;
+};
+hipError_t launch_compact(const CompactLaunch& a, hipStream_t s);
+
+hipError_t launch_crc14(const uint8_t* msg, const int32_t* nbits, int n, uint16_t* crc, hipStream_t s);
+hipError_t launch_ldpc_check(const uint8_t* bits, int n, int32_t* err, hipStream_t s);
+
+}  // namespace ft8

@@ -1,0 +1,168 @@
+/*
+ * ft8hip.h -- C-ABI of libft8hip.so, the MI355X (gfx950) FT8 receive path.
+ *
+ * Drop-in boundary for the reference's Python decoder (Rintazero/ft8_demodulator,
+ * src/ft8_tools/ft8_demodulator).  The reference has no native FFI of its own: every entry point
+ * below replaces one Python function on its decode path, cited as file:line relative to
+ * src/ft8_tools/ft8_demodulator/.  The Python host layer (ft8_demodulator_amd/) binds these with
+ * ctypes and mirrors the reference's functions, names, arguments and error behaviour.
+ *
+ * Conventions
+ *   - All data pointers are device pointers owned by the caller (e.g. torch data_ptr()).  The
+ *     library allocates scratch only inside its context and frees only what it allocated.
+ *   - Every call is asynchronous on the caller's hipStream_t (passed as void*, NULL = default
+ *     stream).  Results are valid after the stream is synchronised.
+ *   - Return 0 (FT8_OK) on success, a negative FT8_E_* code otherwise; ft8_last_error() gives the
+ *     message.  No C++ exception crosses this boundary.
+ *   - One context per device per host thread/stream; a context is not re-entrant.
+ */
+#ifndef FT8HIP_H
+#define FT8HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FT8HIP_ABI_VERSION 1
+
+/* sample dtypes.  The waterfall dtype follows NumPy promotion against complex64 exactly as
+ * scipy.signal.spectrogram does (spectrogram_analyse.py:46-56): F32/C64/I16 -> float32 waterfall,
+ * F64/C128 -> float64 waterfall.  I16 samples are scaled x/32767 in float32 on the device
+ * (from_wave.py:59-67 read_wave_file). */
+enum ft8_dtype { FT8_F32 = 0, FT8_F64 = 1, FT8_C64 = 2, FT8_C128 = 3, FT8_I16 = 4 };
+
+enum ft8_status {
+  FT8_OK = 0,
+  FT8_E_ARG = -1,         /* invalid argument (message in ft8_last_error) */
+  FT8_E_HIP = -2,         /* HIP runtime error */
+  FT8_E_UNSUPPORTED = -3, /* e.g. an FFT length with a prime factor other than 2,3,5,7 */
+  FT8_E_NOMEM = -4,       /* device allocation failed */
+  FT8_E_RANGE = -5        /* a size exceeds a compiled limit (see ft8_limits) */
+};
+
+/* flags */
+#define FT8_FLAG_TOPK 1 /* opt-in true top-k candidate selection (NOT the reference semantics) */
+
+/* Decoder parameters.  Mirrors decode_ft8_message's keyword arguments (ft8_decode.py:288-296);
+ * the freq/time masks (ft8_decode.py:322-341) arrive as index ranges computed on the host. */
+typedef struct ft8_params {
+  int32_t sample_rate;      /* Hz */
+  int32_t bins_per_tone;    /* freq_osr */
+  int32_t steps_per_symbol; /* time_osr */
+  int32_t max_candidates;   /* N of ft8_find_candidates */
+  int32_t max_iterations;   /* BP iterations */
+  int32_t min_score_f64;    /* 1: compare scores with min_score in float64 even for a float32
+                               waterfall (the threshold was an np.float64); 0: in the waterfall
+                               dtype (a Python int/float threshold, NumPy-2 rules) */
+  double min_score;
+  int32_t f_lo, f_hi;       /* kept STFT bins [f_lo, f_hi) after f >= 0 and the band mask */
+  int32_t t_lo, t_hi;       /* kept frames [t_lo, t_hi) after the time mask */
+  int32_t flags;            /* FT8_FLAG_* */
+  int32_t reserved;
+} ft8_params;
+
+/* One decoded (or attempted) candidate, 40 bytes, 8-byte aligned. */
+typedef struct ft8_result {
+  double score;            /* sync score; float32 value widened exactly on the float32 path */
+  int32_t slot;            /* slot index within the batch */
+  int32_t abs_time;        /* candidate time index (frame steps, may be negative) */
+  int32_t abs_freq;        /* candidate frequency index (bins from f_lo) */
+  uint16_t crc_extracted;  /* FT8DecodeStatus.crc_extracted */
+  uint16_t crc_calculated; /* FT8DecodeStatus.crc_calculated (== FT8Message.hash when ok) */
+  int16_t ldpc_errors;     /* FT8DecodeStatus.ldpc_errors (min parity errors seen by BP) */
+  uint16_t cand_index;     /* position in the reference candidate order */
+  uint8_t payload[10];     /* FT8Message.payload (77 bits, [9] & 0xF8) */
+  uint8_t ok;              /* 1: LDPC converged and CRC matched (ft8_decode_candidate True) */
+  uint8_t pad;
+} ft8_result;
+
+typedef struct ft8_ctx ft8_ctx;
+
+/* ---- context ------------------------------------------------------------------------------ */
+int ft8_create(int device, ft8_ctx** out);
+int ft8_destroy(ft8_ctx* ctx);
+const char* ft8_last_error(const ft8_ctx* ctx);
+int ft8_abi_version(void);
+/* compiled limits: max_candidates, max FFT length (real / complex), max records per slot */
+int ft8_limits(int32_t* max_candidates, int32_t* max_fft_real, int32_t* max_fft_complex);
+
+/* STFT geometry of calculate_spectrogram (spectrogram_analyse.py:31-43): window length,
+ * hop, FFT length and frame count for n_samples (frames = 0 when n_samples < nperseg). */
+int ft8_geometry(int32_t sample_rate, int32_t bins_per_tone, int32_t steps_per_symbol,
+                 int64_t n_samples, int32_t* nperseg, int32_t* hop, int32_t* nfft,
+                 int32_t* n_frames);
+
+/* ---- stage 1: STFT -> dB waterfall ---------------------------------------------------------
+ * Replaces calculate_spectrogram (spectrogram_analyse.py:19-66) + the f>=0 / band / time masks
+ * (ft8_decode.py:322-341).  d_samples: n_slots rows of n_samples, row stride slot_stride
+ * elements.  Output d_wf[n_slots][t_hi-t_lo][f_hi-f_lo] (TIME-major: the transpose of the
+ * reference's mag[freq, time]), bins in natural FFT order k in [f_lo, f_hi) of [0, nfft).  For
+ * real input bins above nfft/2 are the mirror image (two-sided spectrum of a real signal). */
+int ft8_stft(ft8_ctx* ctx, const void* d_samples, int dtype, int64_t n_samples, int32_t n_slots,
+             int64_t slot_stride, const ft8_params* p, void* d_wf, void* stream);
+
+/* ---- stage 2: Costas sync score grid + candidate selection ---------------------------------
+ * Replaces ft8_sync_score / ft8_find_candidates (ft8_decode.py:47-149).  d_wf as produced by
+ * ft8_stft: [n_slots][T][F] (row stride F, slot stride T*F), float32 (wf_f64=0) or float64.
+ * Outputs per slot s: d_cand[s][max_candidates][2] = (abs_time, abs_freq) in the reference's
+ * final order, d_cand_score[s][max_candidates] (double), d_cand_count[s].  d_scores (nullable)
+ * receives the full score grid [n_slots][NT][NF] in scan order in the waterfall dtype. */
+int ft8_sync_select(ft8_ctx* ctx, const void* d_wf, int wf_f64, int32_t n_slots, int32_t T,
+                    int32_t F, const ft8_params* p, int32_t* d_cand, double* d_cand_score,
+                    int32_t* d_cand_count, void* d_scores, void* stream);
+
+/* ---- stage 3: soft LLRs --------------------------------------------------------------------
+ * Replaces ft8_extract_likelihood + ftx_normalize_logl (ft8_decode.py:151-198).  d_cand[n][3] =
+ * (slot, abs_time, abs_freq).  Output d_llr[n][174] (double). */
+int ft8_llr(ft8_ctx* ctx, const void* d_wf, int wf_f64, int32_t T, int32_t F,
+            int32_t steps_per_symbol, int32_t bins_per_tone, const int32_t* d_cand, int32_t n,
+            int normalize, double* d_llr, void* stream);
+
+/* ftx_normalize_logl alone (ft8_decode.py:190-198): d_out[n][174] = d_in * sqrt(24 / var(d_in)),
+ * with NumPy's pairwise summation order for the mean and variance. */
+int ft8_normalize(ft8_ctx* ctx, const double* d_in, int32_t n, double* d_out, void* stream);
+
+/* ---- stage 4: LDPC belief propagation + CRC ------------------------------------------------
+ * Replaces bp_decode (ldpc_decoder.py:54-113) and the tail of ft8_decode_candidate
+ * (ft8_decode.py:236-273, crc.py:11-54).  d_llr[n][174] double.  Outputs (each nullable):
+ * d_plain[n][174] hard decisions of the last evaluated iteration, d_res[n] records (score/slot/
+ * abs_* left 0). */
+int ft8_bp(ft8_ctx* ctx, const double* d_llr, int32_t n, int32_t max_iterations,
+           uint8_t* d_plain, ft8_result* d_res, void* stream);
+
+/* ---- whole receive path ---------------------------------------------------------------------
+ * Replaces decode_ft8_message (ft8_decode.py:288-394) for a batch of independent slots:
+ * STFT -> sync/select -> LLR -> BP -> CRC, all on the device.  Writes, per slot s, the successful
+ * decodes in candidate order to d_out[s][0 .. d_counts[s]) (capped at max_results_per_slot;
+ * d_counts holds the uncapped count). */
+int ft8_decode_batch(ft8_ctx* ctx, const void* d_samples, int dtype, int64_t n_samples,
+                     int32_t n_slots, int64_t slot_stride, const ft8_params* p,
+                     ft8_result* d_out, int32_t* d_counts, int32_t max_results_per_slot,
+                     void* stream);
+
+/* Per-slot flags of the last selection (copied device->device into d_out[n_slots]):
+ * bit 0: an exact score tie reached a heap comparison (the reference raises TypeError there,
+ *        ftx_types.py:37-47; here ties are ordered by scan index), bit 1: more new-maximum records
+ *        than kept, tie order approximate. */
+int ft8_select_warnings(ft8_ctx* ctx, int32_t* d_out, int32_t n_slots, void* stream);
+
+/* ---- small device utilities used by the Python mirror of crc.py / ldpc_check ---------------- */
+/* CRC-14 (crc.py:11-39) of d_msg[n][12] over d_nbits[n] bits -> d_crc[n]. */
+int ft8_crc14(ft8_ctx* ctx, const uint8_t* d_msg, const int32_t* d_nbits, int32_t n,
+              uint16_t* d_crc, void* stream);
+/* parity-check error count (ldpc_decoder.py:33-52) of d_bits[n][174] (0/1) -> d_errors[n]. */
+int ft8_ldpc_check(ft8_ctx* ctx, const uint8_t* d_bits, int32_t n, int32_t* d_errors,
+                   void* stream);
+
+/* ---- per-stage device timing (HIP events on the caller's stream) --------------------------- */
+#define FT8_N_STAGES 6 /* 0 stft, 1 score, 2 select, 3 llr+bp, 4 compact, 5 whole decode_batch */
+int ft8_set_timing(ft8_ctx* ctx, int enable);
+/* accumulated milliseconds and launch counts per stage since the last reset; synchronises. */
+int ft8_get_timing(ft8_ctx* ctx, double* ms, int64_t* launches, int reset);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FT8HIP_H */

@@ -1,0 +1,30 @@
+"""The C-ABI library loads and exports every entry point include/ft8hip.h declares (CPU only)."""
+import ctypes
+import os
+import re
+
+from conftest import ROOT
+
+
+def _declared():
+    src = open(os.path.join(ROOT, "include", "ft8hip.h")).read()
+    return sorted(set(re.findall(r"^(?:int|const char\*)\s+(ft8_\w+)\(", src, flags=re.M)))
+
+
+def test_header_symbols_exported():
+    from ft8_demodulator_amd import _lib
+    L = ctypes.CDLL(_lib.LIB_PATH)
+    names = _declared()
+    assert len(names) >= 17
+    for n in names:
+        assert hasattr(L, n), n
+    assert set(names) == set(_lib.EXPORTED_SYMBOLS)
+
+
+def test_host_entry_points_without_gpu():
+    from ft8_demodulator_amd import _lib
+    assert _lib.lib().ft8_abi_version() == 1
+    assert _lib.geometry(12000, 2, 2, 180000) == (1920, 960, 3840, 186)
+    assert _lib.geometry(20000, 2, 2, 252800) == (3200, 1600, 6400, 157)
+    assert _lib.geometry(12000, 2, 2, 1000)[3] == 0
+    assert _lib.limits()["max_candidates"] == 4096
