@@ -1,0 +1,207 @@
+"""Benchmark: 15-s FT8 slots/s (full decode) on MI355X, BASELINE.json config 3 per GPU.
+
+One step = one ft8_decode_batch over a batch of 256 independent synthetic 15-s slots at 12 kHz
+(50 GFSK signals per slot at SNR U(-24, -10) dB, full-band convention; K=300, min_score=2,
+20 BP iterations): STFT -> Costas sync -> selection -> LLR -> BP -> CRC, samples already
+resident in HBM.  With N > 1 GPUs each rank decodes its own 256 slots (weak scaling) and the
+step ends with an RCCL all-gather of every rank's result records (the path's one exchange).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--slots S] [--no-cpu]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+Prints ONE JSON line on rank 0.  Besides the contract fields it carries:
+  roofline      the dominant kernel (k_bp: LLR + float64 BP + CRC), FLOP-rate vs the FP64 vector peak
+  roofline_hbm  the HBM-bound STFT kernel, GB/s vs the 8 TB/s HBM peak
+  stages_ms     per-kernel device time per step (HIP events on the decode stream)
+  cpu_baseline  the oracle port (oracle/, C + scipy) on a bounded sample of the same slots (rank 0, N=1)
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "15-s FT8 slots/sec (full decode) + LDPC candidates/sec, 1/2/4/8 MI355X"
+FP64_VECTOR_PEAK_TFLOPS = 78.6   # MI355X FP64 vector (AMD spec; k_bp issues no MFMA)
+HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def bp_flops_per_pass():
+    """Algorithmic float64 FLOPs of one message-passing sweep of bp_decode (ldpc_decoder.py:88-108):
+    per edge V->C: 2 adds + 1 scale + fast_tanh (x^2, 4 num, 4 den, 1 div) = 13;
+    per edge C->V: (deg-1) products + fast_atanh (10) + 1 scale; plus the per-iteration hard
+    decision (3 adds per bit, counted separately)."""
+    from ft8_demodulator_amd import _ldpc_tables as T
+    f = 0
+    for m in range(83):
+        d = T.CHK_START[m + 1] - T.CHK_START[m]
+        f += d * 13 + d * ((d - 1) + 10 + 1)
+    return f
+
+
+def cpu_worker(args):
+    import numpy as np  # noqa: F401
+    from oracle import oracle as O
+    x, kw = args
+    return len(O.decode_ft8_message(x, 12000, **kw))
+
+
+def cpu_baseline(kw, n_slots, procs, seed, signals):
+    """Oracle port on `n_slots` slots of the benchmark workload, `procs` worker processes.
+
+    Runs before this process touches the GPU, so the workers inherit no device state.  The slots
+    use the same per-slot seeds (payloads, frequencies, start times, SNRs) as the first slots of
+    rank 0's GPU batch; their noise comes from the CPU generator, so the samples are the same
+    workload, not the same bytes."""
+    import multiprocessing as mp
+    from ft8_demodulator_amd import synth
+    from oracle import oracle as O
+    O.lib()
+    x, _ = synth.make_slots(n_slots, signals, fs=12000, snr_db=(-24.0, -10.0), seed=seed, device="cpu")
+    xs = [x[i].numpy() for i in range(n_slots)]
+    ctx = mp.get_context("fork")
+    with ctx.Pool(procs) as pool:
+        pool.map(cpu_worker, [(xs[0], kw)] * procs)  # warm the workers (imports, scipy plans)
+        t0 = time.perf_counter()
+        pool.map(cpu_worker, [(x, kw) for x in xs], chunksize=1)
+        dt = time.perf_counter() - t0
+    return {"value": n_slots / dt, "unit": "slots/s", "cores": procs, "kind": "port",
+            "sample": f"{n_slots} slots of the benchmark workload (same per-slot seeds, K=300, min_score=2, "
+                      f"20 iters); "
+                      f"oracle/ft8_oracle.c + scipy STFT, {procs} processes, {dt:.2f} s wall",
+            "wall_s": dt}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--slots", type=int, default=256, help="slots per GPU per step")
+    ap.add_argument("--signals", type=int, default=50)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-slots", type=int, default=256)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    kw = dict(max_candidates=300, min_score=2, max_iterations=20)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        procs = max(1, min(16, len(os.sched_getaffinity(0))))
+        cpu = cpu_baseline(kw, min(args.cpu_slots, args.slots), procs, 100000, args.signals)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=dev)
+
+    from ft8_demodulator_amd import SlotDecoder, synth
+    from ft8_demodulator_amd.distributed import gather_records
+
+    S = args.slots
+    x, _ = synth.make_slots(S, args.signals, fs=12000, snr_db=(-24.0, -10.0), seed=100000 * (rank + 1),
+                            device=dev)
+    torch.cuda.synchronize()
+    dec = SlotDecoder(12000, 2, 2, device=dev, **kw)
+    ctx = dec.ctx
+
+    def step():
+        out, counts = dec.run(x)
+        if world > 1:
+            gather_records(out, counts)
+        return counts
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    ctx.set_timing(True)
+    ctx.timing(reset=True)
+    ctx.counters(reset=True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        counts = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    ctx.set_timing(False)
+    tm = ctx.timing(reset=True)
+    cn = ctx.counters(reset=True)
+    decoded = int(counts.sum().item())
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        d = torch.tensor([decoded], dtype=torch.int64, device=dev)
+        dist.all_reduce(d)
+        decoded = int(d.item())
+
+    total_slots = S * world * args.steps
+    value = total_slots / elapsed
+    K = args.steps
+    # per-kernel device time (this rank), per step
+    stage_ms = {k: (v[0] / max(v[1], 1)) for k, v in tm.items() if v[1] > 0}
+    bp_ms = stage_ms.get("llr_bp", float("nan"))
+    stft_ms = stage_ms.get("stft", float("nan"))
+    # dominant kernel: k_bp.  Algorithmic FLOPs per launch from the device counters.
+    f_pass = bp_flops_per_pass()
+    f_hd = 174 * 3
+    flops = (cn["passes"] * f_pass + cn["iterations"] * f_hd) / K
+    ach_tf = flops / (bp_ms * 1e-3) / 1e12
+    # STFT: samples read once (f32) + dB waterfall written once
+    from ft8_demodulator_amd._pipeline import make_plan
+    plan = make_plan(x.shape[1], 12000)
+    stft_bytes = S * (x.shape[1] * 4 + plan.T * plan.F * 4)
+    stft_gbs = stft_bytes / (stft_ms * 1e-3) / 1e9
+    cand_per_s = cn["candidates"] / K * world / (elapsed / K)
+
+    line = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "slots/s",
+        "n_gpus": world,
+        "steps": K,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / K * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32 (STFT, sync score) / f64 (LLR, BP)",
+        "data": "synthetic (ft8_demodulator_amd.synth: 50 GFSK signals/slot, SNR U(-24,-10) dB, unit noise)",
+        "config": {"workload": "BASELINE config 3: batch of 256 independent 15-s slots per GPU, 12 kHz, "
+                               "K=300 candidates, min_score=2, 20 BP iterations (config 5 shape at N>1)",
+                   "slots_per_gpu": S, "sample_rate": 12000, "samples_per_slot": int(x.shape[1]),
+                   "max_candidates": 300, "min_score": 2, "max_iterations": 20,
+                   "parallelism": f"slot-sharded x{world}, RCCL all-gather of result records"},
+        "ldpc_candidates_per_s": cand_per_s,
+        "decodes_per_step": decoded / K,
+        "roofline": {"kernel": "k_bp (LLR + float64 BP + CRC)", "bound": "fp64-valu",
+                     "achieved": ach_tf, "peak": FP64_VECTOR_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": ach_tf / FP64_VECTOR_PEAK_TFLOPS, "traffic": None,
+                     "flops_per_launch": flops, "launch_ms": bp_ms,
+                     "bp_passes_per_launch": cn["passes"] / K, "candidates_per_launch": cn["candidates"] / K},
+        "roofline_hbm": {"kernel": "k_stft", "bound": "hbm", "achieved": stft_gbs, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": stft_gbs / HBM_PEAK_GBS, "traffic": None,
+                         "bytes_per_launch": stft_bytes, "launch_ms": stft_ms},
+        "stages_ms": stage_ms,
+        "cpu_baseline": cpu,
+    }
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

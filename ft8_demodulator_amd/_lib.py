@@ -81,6 +81,7 @@ def lib():
             "ft8_ldpc_check": ([vp, vp, i32, vp, vp], ctypes.c_int),
             "ft8_set_timing": ([vp, ctypes.c_int], ctypes.c_int),
             "ft8_get_timing": ([vp, vp, vp, ctypes.c_int], ctypes.c_int),
+            "ft8_get_counters": ([vp, vp, ctypes.c_int], ctypes.c_int),
         }
         for name, (args, res) in sig.items():
             fn = getattr(L, name)
@@ -94,7 +95,7 @@ def lib():
 EXPORTED_SYMBOLS = (
     "ft8_create", "ft8_destroy", "ft8_last_error", "ft8_abi_version", "ft8_limits", "ft8_geometry",
     "ft8_stft", "ft8_sync_select", "ft8_llr", "ft8_normalize", "ft8_bp", "ft8_decode_batch", "ft8_select_warnings",
-    "ft8_crc14", "ft8_ldpc_check", "ft8_set_timing", "ft8_get_timing")
+    "ft8_crc14", "ft8_ldpc_check", "ft8_set_timing", "ft8_get_timing", "ft8_get_counters")
 
 
 def limits():
@@ -154,6 +155,11 @@ class Context:
         cnt = (ctypes.c_int64 * N_STAGES)()
         self.check(lib().ft8_get_timing(self.handle, ms, cnt, int(reset)), "ft8_get_timing")
         return {STAGE_NAMES[i]: (ms[i], cnt[i]) for i in range(N_STAGES)}
+
+    def counters(self, reset: bool = False):
+        v = (ctypes.c_int64 * 4)()
+        self.check(lib().ft8_get_counters(self.handle, v, int(reset)), "ft8_get_counters")
+        return {"candidates": v[0], "iterations": v[1], "passes": v[2], "converged": v[3]}
 
     def __del__(self):
         try:

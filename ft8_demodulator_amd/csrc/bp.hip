@@ -133,6 +133,7 @@ struct BpArgs {
   uint8_t* plain_out;
   ft8_result* res;
   unsigned* work;
+  unsigned long long* stats;  // nullable: [candidates, iterations entered, message passes, converged]
 };
 
 struct WaveLds {
@@ -252,7 +253,9 @@ __global__ __launch_bounds__(kWave) void k_bp(BpArgs a) {
     for (int n = lane; n < FT8_LDPC_N + 2; n += kWave) L.bits[n] = 0;
     __syncthreads();
     int min_errors = FT8_LDPC_M;
+    int entered = 0, passes = 0;
     for (int iter = 0; iter < a.max_iterations; ++iter) {
+      entered++;
       // hard decision: messages = codeword + sum(tov, axis=1) -> c + ((t0 + t1) + t2)
       int ones = 0;
 #pragma unroll
@@ -307,9 +310,16 @@ __global__ __launch_bounds__(kWave) void k_bp(BpArgs a) {
           L.tov[e] = -2 * fast_atanh(p);
         }
       }
+      passes++;
       __syncthreads();
     }
     __syncthreads();
+    if (a.stats && lane == 0) {
+      atomicAdd(&a.stats[0], 1ull);
+      atomicAdd(&a.stats[1], (unsigned long long)entered);
+      atomicAdd(&a.stats[2], (unsigned long long)passes);
+      if (min_errors == 0) atomicAdd(&a.stats[3], 1ull);
+    }
 
     // ---- outputs ------------------------------------------------------------------------------
     if (a.plain_out)
@@ -436,6 +446,7 @@ hipError_t launch_bp(const BpLaunch& L, hipStream_t s) {
   a.plain_out = L.plain_out;
   a.res = L.res;
   a.work = L.work;
+  a.stats = L.stats;
   hipError_t e = hipMemsetAsync(L.work, 0, sizeof(unsigned), s);
   if (e != hipSuccess) return e;
   const int waves = min(L.n_items, 256 * 24);  // 24 single-wave workgroups per CU

@@ -47,7 +47,7 @@ struct ft8_ctx {
   std::string err;
   std::vector<PlanEntry> plans;
   std::vector<WinEntry> wins;
-  DevBuf wf, scores, cand, cand_score, cand_count, rec_idx, warn, res_all, work;
+  DevBuf wf, scores, cand, cand_score, cand_count, rec_idx, warn, res_all, work, stats;
   bool timing = false;
   std::vector<TimedLaunch> pending;
   std::vector<hipEvent_t> pool;
@@ -434,7 +434,7 @@ int ft8_destroy(ft8_ctx* c) {
   {
     DeviceGuard dg(c->device);
     for (auto* b : {&c->wf, &c->scores, &c->cand, &c->cand_score, &c->cand_count, &c->rec_idx, &c->warn,
-                    &c->res_all, &c->work})
+                    &c->res_all, &c->work, &c->stats})
       if (b->p) (void)hipFree(b->p);
     for (auto& p : c->plans) {
       if (p.tw) (void)hipFree(p.tw);
@@ -547,6 +547,7 @@ int ft8_bp(ft8_ctx* c, const double* d_llr, int32_t n, int32_t max_iterations, u
   L.plain_out = d_plain;
   L.res = d_res;
   L.work = (unsigned*)c->work.p;
+  L.stats = (unsigned long long*)c->stats.p;
   StageTimer tm(c, 3, (hipStream_t)stream);
   hipError_t e = launch_bp(L, (hipStream_t)stream);
   tm.done();
@@ -610,6 +611,7 @@ int ft8_decode_batch(ft8_ctx* c, const void* d_samples, int dtype, int64_t n_sam
   B.max_iterations = p->max_iterations;
   B.res = (ft8_result*)c->res_all.p;
   B.work = (unsigned*)c->work.p;
+  B.stats = (unsigned long long*)c->stats.p;
   StageTimer t3(c, 3, s);
   hipError_t e = launch_bp(B, s);
   t3.done();
@@ -657,6 +659,27 @@ int ft8_ldpc_check(ft8_ctx* c, const uint8_t* d_bits, int32_t n, int32_t* d_erro
 int ft8_set_timing(ft8_ctx* c, int enable) {
   if (!c) return FT8_E_ARG;
   c->timing = enable != 0;
+  if (c->timing && !c->stats.p) {
+    DeviceGuard dg(c->device);
+    int rc = ensure(c, c->stats, 4 * sizeof(unsigned long long));
+    if (rc) return rc;
+    hipError_t e = hipMemset(c->stats.p, 0, 4 * sizeof(unsigned long long));
+    if (e != hipSuccess) return hipfail(c, e, "stats reset");
+  }
+  return FT8_OK;
+}
+
+int ft8_get_counters(ft8_ctx* c, int64_t* out4, int reset) {
+  if (!c || !out4) return FT8_E_ARG;
+  for (int i = 0; i < 4; ++i) out4[i] = 0;
+  if (!c->stats.p) return FT8_OK;
+  DeviceGuard dg(c->device);
+  unsigned long long v[4];
+  hipError_t e = hipDeviceSynchronize();
+  if (e == hipSuccess) e = hipMemcpy(v, c->stats.p, sizeof(v), hipMemcpyDeviceToHost);
+  if (e == hipSuccess && reset) e = hipMemset(c->stats.p, 0, sizeof(v));
+  if (e != hipSuccess) return hipfail(c, e, "counters");
+  for (int i = 0; i < 4; ++i) out4[i] = (int64_t)v[i];
   return FT8_OK;
 }
 

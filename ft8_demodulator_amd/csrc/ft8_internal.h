@@ -92,6 +92,7 @@ struct BpLaunch {
   uint8_t* plain_out;      // nullable [n_items][174]
   ft8_result* res;         // nullable [n_items]
   unsigned* work;          // work counter (zeroed by the launcher)
+  unsigned long long* stats = nullptr;  // [candidates, iterations entered, message passes, converged]
 };
 hipError_t launch_bp(const BpLaunch& a, hipStream_t s);
 

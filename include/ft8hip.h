@@ -161,6 +161,9 @@ int ft8_ldpc_check(ft8_ctx* ctx, const uint8_t* d_bits, int32_t n, int32_t* d_er
 int ft8_set_timing(ft8_ctx* ctx, int enable);
 /* accumulated milliseconds and launch counts per stage since the last reset; synchronises. */
 int ft8_get_timing(ft8_ctx* ctx, double* ms, int64_t* launches, int reset);
+/* BP work counters, accumulated while timing is enabled: out4 = {candidates decoded, BP
+ * iterations entered, message-passing sweeps executed, candidates converged}; synchronises. */
+int ft8_get_counters(ft8_ctx* ctx, int64_t* out4, int reset);
 
 #ifdef __cplusplus
 }
