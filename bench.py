@@ -152,7 +152,7 @@ def main():
     K = args.steps
     # per-kernel device time (this rank), per step
     stage_ms = {k: (v[0] / max(v[1], 1)) for k, v in tm.items() if v[1] > 0}
-    bp_ms = stage_ms.get("llr_bp", float("nan"))
+    bp_ms = stage_ms.get("bp", float("nan"))
     stft_ms = stage_ms.get("stft", float("nan"))
     # dominant kernel: k_bp.  Algorithmic FLOPs per launch from the device counters.
     f_pass = bp_flops_per_pass()
@@ -186,7 +186,7 @@ def main():
                    "parallelism": f"slot-sharded x{world}, RCCL all-gather of result records"},
         "ldpc_candidates_per_s": cand_per_s,
         "decodes_per_step": decoded / K,
-        "roofline": {"kernel": "k_bp (LLR + float64 BP + CRC)", "bound": "fp64-valu",
+        "roofline": {"kernel": "k_bp (float64 BP + CRC)", "bound": "fp64-valu",
                      "achieved": ach_tf, "peak": FP64_VECTOR_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": ach_tf / FP64_VECTOR_PEAK_TFLOPS, "traffic": None,
                      "flops_per_launch": flops, "launch_ms": bp_ms,

@@ -34,21 +34,30 @@ __constant__ int kGrayD[8] = {0, 1, 3, 2, 5, 6, 4, 7};  // ft8_decode.py:39
 constexpr int kEdgeSlots = (FT8_LDPC_E + kWave - 1) / kWave;  // 9
 constexpr int kVarSlots = (FT8_LDPC_N + kWave - 1) / kWave;   // 3
 constexpr int kChkSlots = (FT8_LDPC_M + kWave - 1) / kWave;   // 2
+// Every lane owns kEdgeSlots edges, kVarSlots bits and kChkSlots checks; the tails are padded with
+// dummy edges/bits/checks that read and write only padding slots of the LDS arrays, so the three
+// phases are branch-free and the per-lane chains (18 IEEE divisions per sweep) interleave.
+constexpr int kEdgePad = kEdgeSlots * kWave;   // 576: tov/toc slots 522.. are padding
+constexpr int kVarPad = kVarSlots * kWave;     // 192: c/bits slots 174.. are padding
 
-__device__ __forceinline__ double fast_tanh(double x) {  // ldpc_decoder.py:11-21
-  x = x < -4.97 ? -4.97 : x;
-  x = x > 4.97 ? 4.97 : x;
-  const double x2 = x * x;
-  const double a = x * (945.0 + x2 * (105.0 + x2));
-  const double b = 945.0 + x2 * (420.0 + x2 * 15.0);
-  return a / b;
-}
-__device__ __forceinline__ double fast_atanh(double x) {  // ldpc_decoder.py:23-31
-  const double x2 = x * x;
-  const double a = x * (945.0 + x2 * (-735.0 + x2 * 64.0));
-  const double b = (945.0 + x2 * (-1050.0 + x2 * 225.0));
-  return a / b;
-}
+#ifndef BP_DIV_GROUP
+#define BP_DIV_GROUP 3
+#endif
+constexpr int kDivGroup = BP_DIV_GROUP;  // divisions interleaved at a time (kEdgeSlots % kDivGroup == 0)
+#ifndef BP_PROD_GROUP
+#define BP_PROD_GROUP 3
+#endif
+constexpr int kProdGroup = BP_PROD_GROUP;
+#ifndef BP_WAVES_PER_EU
+#define BP_WAVES_PER_EU 4
+#endif
+#ifndef BP_GRID_CUS
+#define BP_GRID_CUS 256  // CUs the persistent grid covers (experiments only)
+#endif
+
+// LDS address-space view of a byte address (the product-factor reads compute raw LDS addresses)
+typedef __attribute__((address_space(3))) const double lds_f64;
+typedef __attribute__((address_space(3))) const uint64_t lds_u64;
 
 // correctly rounded sqrt (math.sqrt): hardware estimate + Tuckerman's test with exact fma residuals
 __device__ double sqrt_rn(double x) {
@@ -72,52 +81,153 @@ __device__ __forceinline__ double pymax4(double a, double b, double c, double d)
   return m;
 }
 
-struct WaveTables {
-  uint32_t vc[kEdgeSlots];   // var n | other edge a << 8 | other edge b << 18
-  uint32_t cv[kEdgeSlots];   // check start | degree << 10 | position << 13
-  uint32_t hd[kVarSlots];    // e0 | e1 << 10 | e2 << 20
-  uint32_t pc[kChkSlots][2]; // variables of the check (8 bits each), up to 7
-  uint32_t pd[kChkSlots];    // degree (0 if slot unused)
+// IEEE-754 double division, the exact instruction sequence hipcc emits for `x / y` on gfx950
+// (div_scale x2, rcp, two Newton steps, mul, fma, div_fmas, div_fixup), written with builtins so
+// that N independent divisions can be interleaved stage by stage (ILP N) with bit-identical results.
+//
+// Fast path: v_div_scale_f64 returns its operand unchanged (VCC = 0) unless the denominator is
+// zero / denormal / has a denormal reciprocal, the quotient is denormal, the exponents differ by
+// >= 768, or the numerator's biased exponent is <= 53 (|x| < 2^-969); v_div_fixup_f64 returns the
+// quotient unchanged for finite normal operands and quotient.  Every denominator here lies in
+// [67, 2.1e4] (fast_tanh: 945 + x^2 (420 + 15 x^2) with |x| <= 4.97; fast_atanh: 945 + x^2 (-1050 +
+// 225 x^2) with |x| <= 1.0072^6) and every numerator below 2.1e4, so when every numerator of the
+// wave satisfies |x| >= 2^-960 the scale/fmas/fixup steps are identities and the short sequence below produces the same
+// bits (measured: ~59 vs ~78 SIMD-cycles per wave division).  Otherwise the full sequence runs.
+template <int N>
+__device__ __forceinline__ void div_rn(double* q, const double* x, const double* y) {
+  bool safe = true;  // |x| < 2^900 always holds here (clamped / bounded inputs); NaN fails the test
+#pragma unroll
+  for (int i = 0; i < N; ++i) safe = safe && (__builtin_fabs(x[i]) >= 0x1p-960);
+  double r[N], e[N], m[N];
+  if (__all(safe)) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) r[i] = __builtin_amdgcn_rcp(y[i]);
+#pragma unroll
+    for (int i = 0; i < N; ++i) e[i] = __builtin_fma(-y[i], r[i], 1.0);
+#pragma unroll
+    for (int i = 0; i < N; ++i) r[i] = __builtin_fma(r[i], e[i], r[i]);
+#pragma unroll
+    for (int i = 0; i < N; ++i) e[i] = __builtin_fma(-y[i], r[i], 1.0);
+#pragma unroll
+    for (int i = 0; i < N; ++i) r[i] = __builtin_fma(r[i], e[i], r[i]);
+#pragma unroll
+    for (int i = 0; i < N; ++i) m[i] = x[i] * r[i];
+#pragma unroll
+    for (int i = 0; i < N; ++i) e[i] = __builtin_fma(-y[i], m[i], x[i]);
+#pragma unroll
+    for (int i = 0; i < N; ++i) q[i] = __builtin_fma(e[i], r[i], m[i]);
+    return;
+  }
+  double den[N], num[N];
+  bool f0[N], f1[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) den[i] = __builtin_amdgcn_div_scale(x[i], y[i], false, &f0[i]);
+#pragma unroll
+  for (int i = 0; i < N; ++i) r[i] = __builtin_amdgcn_rcp(den[i]);
+#pragma unroll
+  for (int i = 0; i < N; ++i) num[i] = __builtin_amdgcn_div_scale(x[i], y[i], true, &f1[i]);
+#pragma unroll
+  for (int i = 0; i < N; ++i) e[i] = __builtin_fma(-den[i], r[i], 1.0);
+#pragma unroll
+  for (int i = 0; i < N; ++i) r[i] = __builtin_fma(r[i], e[i], r[i]);
+#pragma unroll
+  for (int i = 0; i < N; ++i) e[i] = __builtin_fma(-den[i], r[i], 1.0);
+#pragma unroll
+  for (int i = 0; i < N; ++i) r[i] = __builtin_fma(r[i], e[i], r[i]);
+#pragma unroll
+  for (int i = 0; i < N; ++i) m[i] = num[i] * r[i];
+#pragma unroll
+  for (int i = 0; i < N; ++i) e[i] = __builtin_fma(-den[i], m[i], num[i]);
+#pragma unroll
+  for (int i = 0; i < N; ++i) q[i] = __builtin_amdgcn_div_fmas(e[i], r[i], m[i], f1[i]);
+#pragma unroll
+  for (int i = 0; i < N; ++i) q[i] = __builtin_amdgcn_div_fixup(q[i], y[i], x[i]);
+  (void)f0;
+}
+
+// One LDS array holds both message sets: a sweep phase loads everything it needs before it stores
+// (the workgroup is one lockstep wave), so toc can overwrite tov in place and vice versa.  Edge
+// position e lives at msg[2e]; msg[2e + 1] is a constant 1.0, which stands in for the missing sixth
+// product factor of a degree-6 check (the companion of its position 5).
+struct WaveLds {
+  double c[kVarPad];
+  double msg[2 * (kEdgePad + 8)];  // tov between sweeps / toc between the two phases of a sweep
+  uint64_t poff[16];               // [k + 7 * (degree == 6)]: byte offsets of the 6 product factors
+  uint64_t ebits[kEdgeSlots + 1];  // hard decision of every edge's variable, one bit per edge
+  uint8_t bits[256];
+  uint8_t a91[16];
 };
 
-__device__ void load_tables(WaveTables& t, int lane) {
+// Per-lane edge tables (registers, loaded once per wave).
+//   vc: variable n | first other edge << 8 | second other edge << 18 | pos2 << 28 | first << 29
+//       (others in the variable's check order; pos2: this edge is the variable's third edge;
+//        first: this edge is the variable's first edge -- it reports the hard decision)
+//   cv: LDS byte address of the check's row (&msg[2 * start]) | LDS address of its poff entry << 16
+//   ck: check start | degree << 10 for the lane's two check slots (degree 0: padding)
+struct WaveTables {
+  uint32_t vc[kEdgeSlots];
+  uint32_t cv[kEdgeSlots];
+  uint32_t ck[kChkSlots];
+};
+
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const void*)p;
+}
+
+// poff[k + 7 * d6] byte f = 16 * (row position of product factor f of the edge at row position k):
+// positions f + (f >= k), ascending (the reference's row order); a degree-6 check's sixth factor
+// is the 1.0 companion of position 5.
+__device__ void init_poff(WaveLds& L, int lane) {
+  if (lane < 14) {
+    const int k = lane % 7, d6 = lane >= 7;
+    uint64_t w = 0;
+    for (int f = 0; f < 6; ++f) {
+      const uint64_t b = (d6 && f == 5) ? 16 * 5 + 8 : 16 * (f + (f >= k));
+      w |= b << (8 * f);
+    }
+    L.poff[lane] = w;
+  }
+}
+
+__device__ void load_tables(WaveTables& t, const WaveLds& L, int lane) {
+  const uint32_t msg0 = lds_addr(&L.msg[0]), poff0 = lds_addr(&L.poff[0]);
 #pragma unroll
   for (int i = 0; i < kEdgeSlots; ++i) {
     const int e = lane + kWave * i;
-    t.vc[i] = 0;
-    t.cv[i] = 0;
     if (e < FT8_LDPC_E) {
       const int n = kEdgeVarD[e];
-      int o[2], k = 0;
+      int o[2], k = 0, pos = 0;
       for (int j = 0; j < 3; ++j) {
         const int ej = kVarEdgeD[3 * n + j];
         if (ej != e) o[k++] = ej;
+        else pos = j;
       }
-      t.vc[i] = (uint32_t)n | ((uint32_t)o[0] << 8) | ((uint32_t)o[1] << 18);
+      t.vc[i] = (uint32_t)n | ((uint32_t)o[0] << 8) | ((uint32_t)o[1] << 18) | ((uint32_t)(pos == 2) << 28) |
+                ((uint32_t)(pos == 0) << 29);
       const int m = kEdgeChkD[e];
       const int s = kChkStartD[m], d = kChkStartD[m + 1] - s;
-      t.cv[i] = (uint32_t)s | ((uint32_t)d << 10) | ((uint32_t)(e - s) << 13);
+      const uint32_t entry = (uint32_t)(e - s) + (d == 6 ? 7u : 0u);
+      t.cv[i] = (msg0 + 16u * (uint32_t)s) | ((poff0 + 8u * entry) << 16);
+    } else {  // padding edge: reads c[174] and msg[522], its check is the padding block at 522
+      t.vc[i] = (uint32_t)FT8_LDPC_N | ((uint32_t)FT8_LDPC_E << 8) | ((uint32_t)FT8_LDPC_E << 18);
+      const uint32_t k = (uint32_t)(e - FT8_LDPC_E) % 7u;
+      t.cv[i] = (msg0 + 16u * (uint32_t)FT8_LDPC_E) | ((poff0 + 8u * k) << 16);
     }
-  }
-#pragma unroll
-  for (int i = 0; i < kVarSlots; ++i) {
-    const int n = lane + kWave * i;
-    t.hd[i] = 0;
-    if (n < FT8_LDPC_N)
-      t.hd[i] = (uint32_t)kVarEdgeD[3 * n] | ((uint32_t)kVarEdgeD[3 * n + 1] << 10) |
-                ((uint32_t)kVarEdgeD[3 * n + 2] << 20);
   }
 #pragma unroll
   for (int i = 0; i < kChkSlots; ++i) {
     const int m = lane + kWave * i;
-    t.pc[i][0] = t.pc[i][1] = 0;
-    t.pd[i] = 0;
+    t.ck[i] = 0;
     if (m < FT8_LDPC_M) {
       const int s = kChkStartD[m], d = kChkStartD[m + 1] - s;
-      t.pd[i] = d;
-      for (int j = 0; j < d; ++j) t.pc[i][j >> 2] |= (uint32_t)kEdgeVarD[s + j] << (8 * (j & 3));
+      t.ck[i] = (uint32_t)s | ((uint32_t)d << 10);
     }
   }
+  // keep the tables in registers: opaque values cannot be rematerialised from memory in the loop
+#pragma unroll
+  for (int i = 0; i < kEdgeSlots; ++i) asm volatile("" : "+v"(t.vc[i]), "+v"(t.cv[i]));
+#pragma unroll
+  for (int i = 0; i < kChkSlots; ++i) asm volatile("" : "+v"(t.ck[i]));
 }
 
 struct BpArgs {
@@ -128,22 +238,12 @@ struct BpArgs {
   const int32_t* cand_count;
   int N, n_items, mode;
   const double* llr_in;
-  int normalize, max_iterations, llr_only;
+  int normalize, max_iterations;
   double* llr_out;
   uint8_t* plain_out;
   ft8_result* res;
   unsigned* work;
   unsigned long long* stats;  // nullable: [candidates, iterations entered, message passes, converged]
-};
-
-struct WaveLds {
-  double c[FT8_LDPC_N];
-  double tov[FT8_LDPC_E];
-  double toc[FT8_LDPC_E];
-  double part[16];
-  uint8_t bits[FT8_LDPC_N + 2];
-  uint8_t a91[12];
-  int flag[2];
 };
 
 // numpy pairwise sum (loops_utils.h.src) of x[0..174): pw(0,80) + pw(80,94), result in lane 0
@@ -195,11 +295,63 @@ __device__ void extract_llr(const BpArgs& a, const T* wf, int at, int af, double
   }
 }
 
-__global__ __launch_bounds__(kWave) void k_bp(BpArgs a) {
+// ---- k_llr: one wave per candidate -> normalised LLRs in global memory ---------------------------
+// modes: 0 per-slot candidate lists (skips ranks >= the slot's count), 1 explicit (slot, t, f) list,
+// 2 normalise given LLRs
+template <typename T>
+__global__ __launch_bounds__(kWave) void k_llr(BpArgs a) {
+  __shared__ double c[FT8_LDPC_N + 2];
+  __shared__ double sq[FT8_LDPC_N + 2];
+  __shared__ double part[16];
+  const int lane = threadIdx.x;
+  const int item = blockIdx.x;
+  if (item >= a.n_items) return;
+  int slot = 0, at = 0, af = 0;
+  if (a.mode == 0) {
+    slot = item / a.N;
+    const int cidx = item % a.N;
+    if (cidx >= a.cand_count[slot]) return;
+    at = a.cand[((int64_t)slot * a.N + cidx) * 2];
+    af = a.cand[((int64_t)slot * a.N + cidx) * 2 + 1];
+  } else if (a.mode == 1) {
+    slot = a.cand[(int64_t)item * 3];
+    at = a.cand[(int64_t)item * 3 + 1];
+    af = a.cand[(int64_t)item * 3 + 2];
+  }
+  if (a.mode == 2) {
+    for (int n = lane; n < FT8_LDPC_N; n += kWave) c[n] = a.llr_in[(int64_t)item * FT8_LDPC_N + n];
+  } else {
+    extract_llr<T>(a, reinterpret_cast<const T*>(a.wf) + (int64_t)slot * a.T * a.F, at, af, c, lane);
+  }
+  __syncthreads();
+  if (a.normalize) {  // ftx_normalize_logl (ft8_decode.py:190-198)
+    const double mean = pairwise174(c, part, lane) / 174.0;
+    for (int n = lane; n < FT8_LDPC_N; n += kWave) {
+      const double d = c[n] - mean;
+      sq[n] = d * d;
+    }
+    __syncthreads();
+    const double var = pairwise174(sq, part, lane) / 174.0;
+    const double nf = sqrt_rn(24.0 / var);
+    for (int n = lane; n < FT8_LDPC_N; n += kWave) c[n] = c[n] * nf;
+    __syncthreads();
+  }
+  for (int n = lane; n < FT8_LDPC_N; n += kWave) a.llr_out[(int64_t)item * FT8_LDPC_N + n] = c[n];
+}
+
+// ---- k_bp: persistent waves, one candidate at a time ----------------------------------------------
+// modes: 0 per-slot candidate lists (records carry slot / abs_time / abs_freq / score), 2 plain LLRs
+__global__ __launch_bounds__(kWave, BP_WAVES_PER_EU) void k_bp(BpArgs a) {
   __shared__ WaveLds L;
   const int lane = threadIdx.x;
   WaveTables tb;
-  load_tables(tb, lane);
+  load_tables(tb, L, lane);
+  init_poff(L, lane);
+  for (int n = lane; n < kVarPad; n += kWave) L.c[n] = 0.0;
+  for (int n = lane; n < 256; n += kWave) L.bits[n] = 0;
+  for (int e = lane; e < kEdgePad + 8; e += kWave) L.msg[2 * e + 1] = 1.0;
+  if (lane == 0) L.ebits[kEdgeSlots] = 0;
+  __syncthreads();
 
   for (;;) {
     unsigned item = 0;
@@ -207,7 +359,6 @@ __global__ __launch_bounds__(kWave) void k_bp(BpArgs a) {
     item = __shfl(item, 0);
     if ((int)item >= a.n_items) break;
 
-    // ---- candidate --------------------------------------------------------------------------
     int slot = 0, at = 0, af = 0, cidx = 0;
     double score = 0.0;
     if (a.mode == 0) {
@@ -217,101 +368,142 @@ __global__ __launch_bounds__(kWave) void k_bp(BpArgs a) {
       at = a.cand[((int64_t)slot * a.N + cidx) * 2];
       af = a.cand[((int64_t)slot * a.N + cidx) * 2 + 1];
       score = a.cand_score[(int64_t)slot * a.N + cidx];
-    } else if (a.mode == 1) {
-      slot = a.cand[(int64_t)item * 3];
-      at = a.cand[(int64_t)item * 3 + 1];
-      af = a.cand[(int64_t)item * 3 + 2];
     }
-
-    // ---- LLRs -------------------------------------------------------------------------------
-    if (a.mode == 2) {
-      for (int n = lane; n < FT8_LDPC_N; n += kWave) L.c[n] = a.llr_in[(int64_t)item * FT8_LDPC_N + n];
-    } else if (a.wf_f64) {
-      extract_llr<double>(a, reinterpret_cast<const double*>(a.wf) + (int64_t)slot * a.T * a.F, at, af, L.c, lane);
-    } else {
-      extract_llr<float>(a, reinterpret_cast<const float*>(a.wf) + (int64_t)slot * a.T * a.F, at, af, L.c, lane);
-    }
-    __syncthreads();
-    if (a.normalize) {  // ftx_normalize_logl (ft8_decode.py:190-198)
-      const double mean = pairwise174(L.c, L.part, lane) / 174.0;
-      for (int n = lane; n < FT8_LDPC_N; n += kWave) {
-        const double d = L.c[n] - mean;
-        L.toc[n] = d * d;
-      }
-      __syncthreads();
-      const double var = pairwise174(L.toc, L.part, lane) / 174.0;
-      const double nf = sqrt_rn(24.0 / var);
-      for (int n = lane; n < FT8_LDPC_N; n += kWave) L.c[n] = L.c[n] * nf;
-      __syncthreads();
-    }
-    if (a.llr_out)
-      for (int n = lane; n < FT8_LDPC_N; n += kWave) a.llr_out[(int64_t)item * FT8_LDPC_N + n] = L.c[n];
-    if (a.llr_only) continue;
+    for (int n = lane; n < FT8_LDPC_N; n += kWave) L.c[n] = a.llr_in[(int64_t)item * FT8_LDPC_N + n];
 
     // ---- belief propagation (ldpc_decoder.py:54-113) ----------------------------------------
-    for (int e = lane; e < FT8_LDPC_E; e += kWave) L.tov[e] = 0.0;
-    for (int n = lane; n < FT8_LDPC_N + 2; n += kWave) L.bits[n] = 0;
+    // One sweep = the reference iteration: hard decision + checks on the current tov, then
+    // variable->check and check->variable messages.  Fused per edge lane: the gather that feeds
+    // the variable->check sum also yields the variable's hard decision (the lane keeps its own
+    // tov in a register), so the decision costs no extra LDS traffic.
+    for (int e = lane; e < kEdgePad + 8; e += kWave) L.msg[2 * e] = 0.0;
+    if (lane <= kEdgeSlots) L.ebits[lane] = 0;  // the hard decision if no sweep runs
     __syncthreads();
+    double tv[kEdgeSlots];
+#pragma unroll
+    for (int i = 0; i < kEdgeSlots; ++i) tv[i] = 0.0;
     int min_errors = FT8_LDPC_M;
     int entered = 0, passes = 0;
     for (int iter = 0; iter < a.max_iterations; ++iter) {
       entered++;
-      // hard decision: messages = codeword + sum(tov, axis=1) -> c + ((t0 + t1) + t2)
-      int ones = 0;
+      // re-opaque the tables every sweep: otherwise the compiler hoists all 90 derived LDS
+      // addresses out of the loop (spilling); recomputing them is a few integer ops
 #pragma unroll
-      for (int i = 0; i < kVarSlots; ++i) {
-        const int n = lane + kWave * i;
-        if (n < FT8_LDPC_N) {
-          const uint32_t h = tb.hd[i];
-          const double sum = (L.tov[h & 1023] + L.tov[(h >> 10) & 1023]) + L.tov[h >> 20];
-          const int b = (L.c[n] + sum) > 0.0;
-          L.bits[n] = (uint8_t)b;
-          ones += b;
+      for (int i = 0; i < kEdgeSlots; ++i) asm volatile("" : "+v"(tb.vc[i]), "+v"(tb.cv[i]));
+#pragma unroll
+      for (int i = 0; i < kChkSlots; ++i) asm volatile("" : "+v"(tb.ck[i]));
+      double x[kEdgeSlots];
+      uint64_t hd[kEdgeSlots];  // wave ballots: hard decision of every edge's variable
+      {
+        double tc[kEdgeSlots], ta[kEdgeSlots], tb2[kEdgeSlots];
+#pragma unroll
+        for (int i = 0; i < kEdgeSlots; ++i) {
+          const uint32_t v = tb.vc[i];
+          tc[i] = L.c[v & 255];
+          ta[i] = L.msg[2 * ((v >> 8) & 1023)];
+          tb2[i] = L.msg[2 * ((v >> 18) & 1023)];
+        }
+#pragma unroll
+        for (int i = 0; i < kEdgeSlots; ++i) {
+          const bool p2 = (tb.vc[i] >> 28) & 1u;
+          // messages = codeword + sum(tov, axis=1): c + ((t0 + t1) + t2) in the variable's order:
+          // own edge first or second -> (own + oa) + ob; own edge third -> (oa + ob) + own
+          const double u = p2 ? tb2[i] : tv[i];
+          const double hs = (ta[i] + u) + (p2 ? tv[i] : tb2[i]);
+          hd[i] = __ballot((tc[i] + hs) > 0.0);
+          // variable -> check input: Tnm = c[n] + other1 + other2 (ldpc_decoder.py:93-96)
+          double t = tc[i];
+          t += ta[i];
+          t += tb2[i];
+          x[i] = __builtin_fmin(__builtin_fmax(-t / 2, -4.97), 4.97);  // np.clip (no NaN reaches here)
         }
       }
-      if (!__any(ones != 0)) break;  // np.sum(plain) == 0
+      // publish the edge bits for the parity check and the final hard decision
+      if (lane == 0) {
+#pragma unroll
+        for (int i = 0; i < kEdgeSlots; ++i) L.ebits[i] = hd[i];
+      }
+      // all-zero hard decision -> stop (ldpc_decoder.py:76-78); padding edges (slot 8, lanes >= 10)
+      // never count
+      uint64_t any = hd[kEdgeSlots - 1] & ((1ull << (FT8_LDPC_E - kWave * (kEdgeSlots - 1))) - 1ull);
+#pragma unroll
+      for (int i = 0; i < kEdgeSlots - 1; ++i) any |= hd[i];
       __syncthreads();
-      // parity check (ldpc_check, ldpc_decoder.py:33-52)
+      if (any == 0) break;
+      // parity check (ldpc_check, ldpc_decoder.py:33-52): a check's edges are contiguous
       int errs = 0;
 #pragma unroll
       for (int i = 0; i < kChkSlots; ++i) {
-        const int d = tb.pd[i];
-        int x = 0;
-        for (int j = 0; j < d; ++j) x ^= L.bits[(tb.pc[i][j >> 2] >> (8 * (j & 3))) & 255];
-        errs += __popcll(__ballot(x != 0));
+        const uint32_t ck = tb.ck[i];
+        const int s0 = ck & 1023, d = ck >> 10;
+        const uint64_t lo = L.ebits[s0 >> 6], hi = L.ebits[(s0 >> 6) + 1];
+        const int sh = s0 & 63;
+        const uint64_t w = sh ? ((lo >> sh) | (hi << (64 - sh))) : lo;
+        const uint64_t bitsd = w & ((1ull << d) - 1ull);
+        errs += __popcll(__ballot(__popcll(bitsd) & 1));
       }
       if (errs < min_errors) {
         min_errors = errs;
         if (errs == 0) break;
       }
-      // variable -> check: toc = tanh(-(c[n] + others) / 2), others in the variable's check order
+      // variable -> check messages: toc = fast_tanh(-Tnm / 2), three interleaved divisions at a time
 #pragma unroll
-      for (int i = 0; i < kEdgeSlots; ++i) {
-        const int e = lane + kWave * i;
-        if (e < FT8_LDPC_E) {
-          const uint32_t v = tb.vc[i];
-          double t = L.c[v & 255];
-          t += L.tov[(v >> 8) & 1023];
-          t += L.tov[v >> 18];
-          L.toc[e] = fast_tanh(-t / 2);
+      for (int g = 0; g < kEdgeSlots; g += kDivGroup) {
+        double na[kDivGroup], nb[kDivGroup];
+#pragma unroll
+        for (int i = 0; i < kDivGroup; ++i) {
+          const double xv = x[g + i], x2 = xv * xv;
+          na[i] = xv * (945.0 + x2 * (105.0 + x2));
+          nb[i] = 945.0 + x2 * (420.0 + x2 * 15.0);
         }
+        div_rn<kDivGroup>(&x[g], na, nb);
       }
+#pragma unroll
+      for (int i = 0; i < kEdgeSlots; ++i) L.msg[2 * (lane + kWave * i)] = x[i];
       __syncthreads();
-      // check -> variable: tov = -2 atanh(prod of the other toc of the check, in row order)
+      // check -> variable messages: tov = -2 fast_atanh(prod of the other toc of the check, in row
+      // order, from 1.0).  The six factor addresses are the row address plus the bytes of the
+      // edge's poff word (one SDWA add each); 1.0 * t0 == t0, so the product starts at factor 0.
 #pragma unroll
       for (int i = 0; i < kEdgeSlots; ++i) {
-        const int e = lane + kWave * i;
-        if (e < FT8_LDPC_E) {
-          const uint32_t v = tb.cv[i];
-          const int s = v & 1023, d = (v >> 10) & 7, k = v >> 13;
-          double p = 1.0;
-          for (int j = 0; j < d; ++j)
-            if (j != k) p *= L.toc[s + j];
-          L.tov[e] = -2 * fast_atanh(p);
+        const uint32_t v = tb.cv[i];
+        const uint64_t pk = *(lds_u64*)(uintptr_t)(v >> 16);
+        const uint32_t row = v & 0xFFFFu;
+        double p = 0.0;
+#pragma unroll
+        for (int f = 0; f < 6; ++f) {
+          const uint32_t off = (uint32_t)(pk >> (8 * f)) & 0xFFu;
+          const double t = *(lds_f64*)(uintptr_t)(row + off);
+          p = f == 0 ? t : p * t;
         }
+        x[i] = p;
+        // bound how far the scheduler hoists these loads (register pressure)
+        if (i % kProdGroup == kProdGroup - 1) asm volatile("" ::: "memory");
+      }
+#pragma unroll
+      for (int g = 0; g < kEdgeSlots; g += kDivGroup) {
+        double na[kDivGroup], nb[kDivGroup];
+#pragma unroll
+        for (int i = 0; i < kDivGroup; ++i) {
+          const double xv = x[g + i], x2 = xv * xv;
+          na[i] = xv * (945.0 + x2 * (-735.0 + x2 * 64.0));
+          nb[i] = (945.0 + x2 * (-1050.0 + x2 * 225.0));
+        }
+        div_rn<kDivGroup>(&x[g], na, nb);
+      }
+#pragma unroll
+      for (int i = 0; i < kEdgeSlots; ++i) {
+        tv[i] = -2 * x[i];
+        L.msg[2 * (lane + kWave * i)] = tv[i];
       }
       passes++;
       __syncthreads();
+    }
+    // hard decision of the last evaluated sweep -> bits[n], reported by each variable's first edge
+#pragma unroll
+    for (int i = 0; i < kEdgeSlots; ++i) {
+      const uint32_t v = tb.vc[i];
+      if ((v >> 29) & 1u) L.bits[v & 255] = (uint8_t)((L.ebits[i] >> lane) & 1u);
     }
     __syncthreads();
     if (a.stats && lane == 0) {
@@ -420,10 +612,7 @@ __global__ void k_ldpc_check(const uint8_t* bits, int n, int32_t* err) {
   err[i] = e;
 }
 
-}  // namespace
-
-hipError_t launch_bp(const BpLaunch& L, hipStream_t s) {
-  if (L.n_items <= 0) return hipSuccess;
+BpArgs make_args(const BpLaunch& L) {
   BpArgs a{};
   a.wf = L.wf;
   a.wf_f64 = L.wf_f64;
@@ -441,15 +630,32 @@ hipError_t launch_bp(const BpLaunch& L, hipStream_t s) {
   a.llr_in = L.llr_in;
   a.normalize = L.normalize;
   a.max_iterations = L.max_iterations;
-  a.llr_only = L.llr_only;
   a.llr_out = L.llr_out;
   a.plain_out = L.plain_out;
   a.res = L.res;
   a.work = L.work;
   a.stats = L.stats;
+  return a;
+}
+
+}  // namespace
+
+hipError_t launch_llr(const BpLaunch& L, hipStream_t s) {
+  if (L.n_items <= 0) return hipSuccess;
+  BpArgs a = make_args(L);
+  if (L.wf_f64)
+    hipLaunchKernelGGL(k_llr<double>, dim3(L.n_items), dim3(kWave), 0, s, a);
+  else
+    hipLaunchKernelGGL(k_llr<float>, dim3(L.n_items), dim3(kWave), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_bp(const BpLaunch& L, hipStream_t s) {
+  if (L.n_items <= 0) return hipSuccess;
+  BpArgs a = make_args(L);
   hipError_t e = hipMemsetAsync(L.work, 0, sizeof(unsigned), s);
   if (e != hipSuccess) return e;
-  const int waves = min(L.n_items, 256 * 24);  // 24 single-wave workgroups per CU
+  const int waves = min(L.n_items, BP_GRID_CUS * 4 * BP_WAVES_PER_EU);  // one resident wave per slot
   hipLaunchKernelGGL(k_bp, dim3(waves), dim3(kWave), 0, s, a);
   return hipGetLastError();
 }

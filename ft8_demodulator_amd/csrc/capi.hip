@@ -47,7 +47,7 @@ struct ft8_ctx {
   std::string err;
   std::vector<PlanEntry> plans;
   std::vector<WinEntry> wins;
-  DevBuf wf, scores, cand, cand_score, cand_count, rec_idx, warn, res_all, work, stats;
+  DevBuf wf, scores, cand, cand_score, cand_count, rec_idx, warn, res_all, work, stats, llr;
   bool timing = false;
   std::vector<TimedLaunch> pending;
   std::vector<hipEvent_t> pool;
@@ -434,7 +434,7 @@ int ft8_destroy(ft8_ctx* c) {
   {
     DeviceGuard dg(c->device);
     for (auto* b : {&c->wf, &c->scores, &c->cand, &c->cand_score, &c->cand_count, &c->rec_idx, &c->warn,
-                    &c->res_all, &c->work, &c->stats})
+                    &c->res_all, &c->work, &c->stats, &c->llr})
       if (b->p) (void)hipFree(b->p);
     for (auto& p : c->plans) {
       if (p.tw) (void)hipFree(p.tw);
@@ -489,8 +489,6 @@ int ft8_llr(ft8_ctx* c, const void* d_wf, int wf_f64, int32_t T, int32_t F, int3
   if (!c || !d_llr || (!d_cand && n > 0) || sps <= 0 || bpt <= 0) return fail(c, FT8_E_ARG, "bad argument");
   if (n <= 0) return FT8_OK;
   DeviceGuard dg(c->device);
-  int rc;
-  if ((rc = ensure(c, c->work, 16))) return rc;
   BpLaunch L{};
   L.wf = d_wf;
   L.wf_f64 = wf_f64;
@@ -502,11 +500,9 @@ int ft8_llr(ft8_ctx* c, const void* d_wf, int wf_f64, int32_t T, int32_t F, int3
   L.n_items = n;
   L.mode = 1;
   L.normalize = normalize;
-  L.llr_only = 1;
   L.llr_out = d_llr;
-  L.work = (unsigned*)c->work.p;
-  StageTimer tm(c, 3, (hipStream_t)stream);
-  hipError_t e = launch_bp(L, (hipStream_t)stream);
+  StageTimer tm(c, 6, (hipStream_t)stream);
+  hipError_t e = launch_llr(L, (hipStream_t)stream);
   tm.done();
   return e == hipSuccess ? FT8_OK : hipfail(c, e, "llr launch");
 }
@@ -515,18 +511,14 @@ int ft8_normalize(ft8_ctx* c, const double* d_in, int32_t n, double* d_out, void
   if (!c || (n > 0 && (!d_in || !d_out))) return fail(c, FT8_E_ARG, "bad argument");
   if (n <= 0) return FT8_OK;
   DeviceGuard dg(c->device);
-  int rc;
-  if ((rc = ensure(c, c->work, 16))) return rc;
   BpLaunch L{};
   L.mode = 2;
   L.llr_in = d_in;
   L.n_items = n;
   L.normalize = 1;
-  L.llr_only = 1;
   L.llr_out = d_out;
-  L.work = (unsigned*)c->work.p;
-  StageTimer tm(c, 3, (hipStream_t)stream);
-  hipError_t e = launch_bp(L, (hipStream_t)stream);
+  StageTimer tm(c, 6, (hipStream_t)stream);
+  hipError_t e = launch_llr(L, (hipStream_t)stream);
   tm.done();
   return e == hipSuccess ? FT8_OK : hipfail(c, e, "normalize launch");
 }
@@ -588,6 +580,7 @@ int ft8_decode_batch(ft8_ctx* c, const void* d_samples, int dtype, int64_t n_sam
   if ((rc = ensure(c, c->cand_score, sizeof(double) * (size_t)n_slots * N))) return rc;
   if ((rc = ensure(c, c->cand_count, sizeof(int32_t) * (size_t)n_slots))) return rc;
   if ((rc = ensure(c, c->res_all, sizeof(ft8_result) * (size_t)n_slots * N))) return rc;
+  if ((rc = ensure(c, c->llr, sizeof(double) * FT8_LDPC_N * (size_t)n_slots * N))) return rc;
   if ((rc = ensure(c, c->work, 16))) return rc;
   if ((rc = do_stft(c, d_samples, dtype, n_samples, n_slots, slot_stride, p, c->wf.p, s))) return rc;
   if ((rc = do_sync_select(c, c->wf.p, f64, n_slots, T, F, p, (int32_t*)c->cand.p, (double*)c->cand_score.p,
@@ -609,11 +602,17 @@ int ft8_decode_batch(ft8_ctx* c, const void* d_samples, int dtype, int64_t n_sam
   B.mode = 0;
   B.normalize = 1;
   B.max_iterations = p->max_iterations;
+  B.llr_out = (double*)c->llr.p;
+  B.llr_in = (const double*)c->llr.p;
   B.res = (ft8_result*)c->res_all.p;
   B.work = (unsigned*)c->work.p;
   B.stats = (unsigned long long*)c->stats.p;
+  StageTimer t6(c, 6, s);
+  hipError_t e = launch_llr(B, s);
+  t6.done();
+  if (e != hipSuccess) return hipfail(c, e, "llr launch");
   StageTimer t3(c, 3, s);
-  hipError_t e = launch_bp(B, s);
+  e = launch_bp(B, s);
   t3.done();
   if (e != hipSuccess) return hipfail(c, e, "bp launch");
   CompactLaunch C{};

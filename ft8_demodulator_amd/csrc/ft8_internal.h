@@ -83,18 +83,18 @@ struct BpLaunch {
   int n_slots;
   int n_items;             // mode B item count, or n_slots*N in mode A
   int mode;                // 0: waterfall+per-slot candidates, 1: waterfall+explicit list,
-                           // 2: LLR input
-  const double* llr_in;    // mode 2
-  int normalize;           // llr stage only
+                           // 2: LLR input (k_llr: normalise only; k_bp: no candidate metadata)
+  const double* llr_in;    // k_bp: always; k_llr: mode 2
+  int normalize;           // k_llr only
   int max_iterations;
-  int llr_only;            // 1: stop after the LLR stage
-  double* llr_out;         // nullable [n_items][174]
+  double* llr_out;         // k_llr output [n_items][174]
   uint8_t* plain_out;      // nullable [n_items][174]
   ft8_result* res;         // nullable [n_items]
   unsigned* work;          // work counter (zeroed by the launcher)
   unsigned long long* stats = nullptr;  // [candidates, iterations entered, message passes, converged]
 };
-hipError_t launch_bp(const BpLaunch& a, hipStream_t s);
+hipError_t launch_llr(const BpLaunch& a, hipStream_t s);  // k_llr: waterfall -> LLRs
+hipError_t launch_bp(const BpLaunch& a, hipStream_t s);   // k_bp: LLRs -> BP + CRC
 
 struct CompactLaunch {
   const ft8_result* res;   // [n_slots][N]

@@ -286,7 +286,7 @@ __global__ __launch_bounds__(kThreads) void k_stft(StftArgs a) {
     const CT pw = (X.x * X.x + X.y * X.y) * scale;
     if constexpr (sizeof(CT) == 4) {
       const float v = 1e-12f + pw;
-      out[i] = 10.0f * (float)log10((double)v);
+      out[i] = 10.0f * log10f(v);
     } else {
       out[i] = 10.0 * log10(1e-12 + pw);
     }

@@ -157,7 +157,7 @@ int ft8_ldpc_check(ft8_ctx* ctx, const uint8_t* d_bits, int32_t n, int32_t* d_er
                    void* stream);
 
 /* ---- per-stage device timing (HIP events on the caller's stream) --------------------------- */
-#define FT8_N_STAGES 6 /* 0 stft, 1 score, 2 select, 3 llr+bp, 4 compact, 5 whole decode_batch */
+#define FT8_N_STAGES 7 /* 0 stft, 1 score, 2 select, 3 bp, 4 compact, 5 whole decode_batch, 6 llr */
 int ft8_set_timing(ft8_ctx* ctx, int enable);
 /* accumulated milliseconds and launch counts per stage since the last reset; synchronises. */
 int ft8_get_timing(ft8_ctx* ctx, double* ms, int64_t* launches, int reset);

@@ -79,7 +79,7 @@ def test_ldpc_tables(oracle):
     src = open(os.path.join(ROOT, "ft8_demodulator_amd", "csrc", "ft8_ldpc_tables.h")).read()
     assert T.SHA256 in src
     assert len(T.EDGE_VAR) == 522 and T.CHK_START[-1] == 522
-    assert sorted(constants.kFTX_LDPC_Num_rows) == [6] * 58 + [7] * 25
+    assert sorted(constants.kFTX_LDPC_Num_rows) == [6] * 59 + [7] * 24  # 59*6 + 24*7 = 522 edges
     # every variable in exactly 3 checks, Mn is the transpose of Nm
     for n, row in enumerate(constants.kFTX_LDPC_Mn):
         assert len(set(row)) == 3
