@@ -47,7 +47,7 @@ struct ft8_ctx {
   std::string err;
   std::vector<PlanEntry> plans;
   std::vector<WinEntry> wins;
-  DevBuf wf, scores, cand, cand_score, cand_count, rec_idx, warn, res_all, work, stats, llr;
+  DevBuf wf, scores, cand, cand_score, cand_count, rec_idx, warn, rowsum, res_all, work, stats, llr;
   bool timing = false;
   std::vector<TimedLaunch> pending;
   std::vector<hipEvent_t> pool;
@@ -369,6 +369,7 @@ int do_sync_select(ft8_ctx* c, const void* d_wf, int wf_f64, int n_slots, int T,
   }
   if ((rc = ensure(c, c->rec_idx, sizeof(int32_t) * (size_t)n_slots * kMaxRecords))) return rc;
   if ((rc = ensure(c, c->warn, sizeof(int32_t) * (size_t)n_slots))) return rc;
+  if ((rc = ensure(c, c->rowsum, sizeof(RowSummary) * (size_t)n_slots * g.NT))) return rc;
   SyncLaunch L{};
   L.wf = d_wf;
   L.wf_f64 = wf_f64;
@@ -390,6 +391,7 @@ int do_sync_select(ft8_ctx* c, const void* d_wf, int wf_f64, int n_slots, int T,
   L.cand_count = cand_count;
   L.rec_idx = (int32_t*)c->rec_idx.p;
   L.warn = (int32_t*)c->warn.p;
+  L.rowsum = (RowSummary*)c->rowsum.p;
   StageTimer t1(c, 1, s);
   hipError_t e = launch_score(L, s);
   t1.done();
@@ -433,7 +435,7 @@ int ft8_destroy(ft8_ctx* c) {
   if (!c) return FT8_OK;
   {
     DeviceGuard dg(c->device);
-    for (auto* b : {&c->wf, &c->scores, &c->cand, &c->cand_score, &c->cand_count, &c->rec_idx, &c->warn,
+    for (auto* b : {&c->wf, &c->scores, &c->cand, &c->cand_score, &c->cand_count, &c->rec_idx, &c->warn, &c->rowsum,
                     &c->res_all, &c->work, &c->stats, &c->llr})
       if (b->p) (void)hipFree(b->p);
     for (auto& p : c->plans) {

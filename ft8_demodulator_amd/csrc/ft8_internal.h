@@ -50,6 +50,23 @@ struct StftLaunch {
 hipError_t launch_stft(const StftLaunch& a, hipStream_t s);
 
 // ---- sync score + selection ----------------------------------------------------------------
+// Per (slot, time row) summary written by k_score for k_select: how many grid points of the row
+// pass the min_score test, and the largest passing score as an order-preserving key (0 = none).
+struct RowSummary {
+  unsigned count;
+  unsigned pad;
+  unsigned long long maxkey;
+};
+__host__ __device__ inline unsigned long long order_key(double v) {
+  union { double d; unsigned long long u; } x{v};
+  return (x.u >> 63) ? ~x.u : (x.u | 0x8000000000000000ull);
+}
+__host__ __device__ inline double key_value(unsigned long long k) {
+  union { double d; unsigned long long u; } x;
+  x.u = (k >> 63) ? (k & 0x7fffffffffffffffull) : ~k;
+  return x.d;
+}
+
 struct SyncLaunch {
   const void* wf;          // [n_slots][T][F]
   int wf_f64;
@@ -67,6 +84,7 @@ struct SyncLaunch {
   int32_t* rec_idx;        // scratch [n_slots][kMaxRecords]
   int32_t* warn;           // scratch [n_slots] (bit 0: tie reached a heap comparison,
                            //                    bit 1: record overflow -> approximate tie order)
+  RowSummary* rowsum;      // scratch [n_slots][NT]: passing count + max passing score per time row
 };
 hipError_t launch_score(const SyncLaunch& a, hipStream_t s);
 hipError_t launch_select(const SyncLaunch& a, hipStream_t s);

@@ -1,30 +1,43 @@
 // sync.hip -- Costas-7 sync score grid and the reference's candidate selection (gfx950).
 //
-// k_score replaces ft8_sync_score over the ft8_find_candidates grid (reference
-// ft8_decode.py:47-100, 108-131; FT8Candidate.get_log_power ftx_types.py:45-47).  Each thread
-// owns one candidate (abs_time, abs_freq) and accumulates its up-to-75 dB differences
-// SEQUENTIALLY in the reference order (m, k, then tone-1, tone+1, time-1, time+1): on the float32
-// waterfall of a WAV the reference sums in np.float32 (NumPy-2 promotion, ft8_decode.py:57,80-94)
-// and any re-association would change the last bit of the score, so the sum is never
-// tree-reduced.  A workgroup covers TW consecutive frequency columns of one slot for every time
-// row of the grid; the waterfall strip it touches (all rows x (TW + 7*bpt) columns, 58 KB at
-// 12 kHz fp32) is staged in LDS once and read conflict-free (lanes = consecutive columns).
-// Geometries whose strip does not fit LDS read through L1/L2 instead (same code path, templated).
+// k_score2 / k_score replace ft8_sync_score over the ft8_find_candidates grid (reference
+// ft8_decode.py:47-100, 108-131; FT8Candidate.get_log_power ftx_types.py:45-47).  Every candidate
+// (abs_time, abs_freq) accumulates its up-to-75 dB differences SEQUENTIALLY in the reference order
+// (m, k, then tone-1, tone+1, time-1, time+1): on the float32 waterfall of a WAV the reference sums
+// in np.float32 (NumPy-2 promotion, ft8_decode.py:57,80-94) and any re-association would change
+// the last bit of the score, so the sum is never tree-reduced.
+//
+// k_score2 (float32 waterfall, bins_per_tone/steps_per_symbol in {1..4}, the production path):
+//   * a workgroup owns 128 frequency columns x 22 time rows of the grid of one slot; it stages the
+//     three Costas bands of the waterfall those candidates touch (3 x (22 + 8 sps) rows x
+//     (128 + 7 bpt) columns, 63 KB at bpt = sps = 2) in LDS once;
+//   * a wave owns one time row at a time (so every range test of the reference is wave-uniform and
+//     compiles to a scalar branch) and each lane two adjacent columns: the pair is accumulated
+//     with packed float32 adds (v_pk_add_f32, two independent IEEE sums) from 8-byte LDS reads
+//     whose addresses are one per-lane base plus compile-time immediates;
+//   * slots map to XCDs (workgroup id % 8), so all tiles of a slot share one L2;
+//   * each wave also folds its row into a per-(slot, row) summary -- passing count and largest
+//     passing score -- which lets k_select skip the rows it does not need.
+// k_score (float64 waterfalls and other oversampling factors) is the plain one-thread-per-
+// candidate form of the same sum.
 //
 // k_select replaces the heap logic of ft8_find_candidates (ft8_decode.py:113-140), one 1024-thread
 // workgroup per slot.  The reference heap stores (-score, cand) and admits a candidate into a full
 // heap only when it beats heap[0] -- the CURRENT MAXIMUM -- which it then evicts.  The selected set
 // is therefore: the first N passing candidates in scan order (time outer, frequency inner), with
-// the maximum of those replaced by each later strict new maximum ("record") in turn.  The kernel
-// finds ranks and records with two block scans (count, running max), sorts the set by score, and
-// only when two selected scores are exactly equal (where the reference's order depends on heap
-// array positions) replays the reference heapq sequence in LDS to reproduce its stable sort.
+// the maximum of those replaced by each later strict new maximum ("record") in turn, i.e. by the
+// first occurrence of the global maximum when that lies beyond rank N.  From the row summaries
+// the kernel finds the rows holding ranks < N and the row of the global maximum, and scans only
+// those; it sorts the set by score, and only when two selected scores are exactly equal (where
+// the reference's order depends on heap array positions) rescans the whole grid for the records
+// and replays the reference heapq sequence in LDS to reproduce its stable sort.
 #include "ft8_internal.h"
 
 namespace ft8 {
 namespace {
 
 __constant__ int kCostasD[7] = {3, 1, 4, 0, 6, 5, 2};  // ft8_decode.py:42
+constexpr int kCostasC[7] = {3, 1, 4, 0, 6, 5, 2};
 
 constexpr int kScoreThreads = 256;
 constexpr size_t kScoreLdsBudget = 64 * 1024;
@@ -35,7 +48,20 @@ struct ScoreArgs {
   int t0, NT, NF;
   int rlo, nrows;    // staged rows [rlo, rlo + nrows)
   void* scores;
+  RowSummary* rowsum;
+  double min_score;
+  int cmp_f64;
+  int n_slots, n_bands, n_ctiles;  // k_score2 grid
 };
+
+// ft8_find_candidates' admission test (ft8_decode.py:127): not -inf and not below min_score, the
+// comparison done in the score's dtype unless min_score is a float64 scalar
+template <typename T>
+__device__ __forceinline__ bool passes(T s, double ms, int cmp_f64) {
+  if (s == (T)-INFINITY) return false;
+  if (cmp_f64) return !((double)s < ms);
+  return !(s < (T)ms);
+}
 
 template <typename T, bool LDS, int TW>
 __global__ __launch_bounds__(kScoreThreads) void k_score(ScoreArgs a) {
@@ -62,6 +88,7 @@ __global__ __launch_bounds__(kScoreThreads) void k_score(ScoreArgs a) {
   constexpr int kGroups = kScoreThreads / TW;
   const int af = c0 + lane_col;
   T* out = reinterpret_cast<T*>(a.scores) + (int64_t)slot * a.NT * a.NF;
+  RowSummary* rs = a.rowsum + (int64_t)slot * a.NT;
   const int sps = a.sps, bpt = a.bpt, nb = a.num_blocks;
   for (int ti = rgroup; ti < a.NT; ti += kGroups) {
     if (af >= a.NF) continue;
@@ -90,7 +117,135 @@ __global__ __launch_bounds__(kScoreThreads) void k_score(ScoreArgs a) {
     if (n == 0 || isnan(score) || isinf(score)) res = (T)-INFINITY;
     else res = score / (T)n;
     out[(int64_t)ti * a.NF + af] = res;
+    if (passes(res, a.min_score, a.cmp_f64)) {
+      atomicAdd(&rs[ti].count, 1u);
+      atomicMax(&rs[ti].maxkey, order_key((double)res));
+    }
   }
+}
+
+// ---- k_score2 ----------------------------------------------------------------------------------
+constexpr int kS2TW = 128;                 // grid columns per workgroup (64 lanes x 2)
+constexpr int kS2R = 22;                   // grid rows per workgroup (88 = 4 x 22 at 12 kHz)
+constexpr int kS2Waves = 11;               // each wave takes rows w, w + 11
+constexpr int kS2Threads = kS2Waves * kWave;
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+template <int BPT, int SPS>
+struct S2Geom {
+  static constexpr int P = kS2TW + 7 * BPT + (BPT & 1);  // staged columns (even: 8-byte rows)
+  static constexpr int H = kS2R + 8 * SPS;               // staged rows per Costas band
+  static constexpr int kFloats = 3 * H * P;
+};
+
+template <int BPT>
+__device__ __forceinline__ f32x2 ld2(const float* p) {
+  if constexpr (BPT % 2 == 0) return *reinterpret_cast<const f32x2*>(p);
+  else return f32x2{p[0], p[1]};
+}
+
+template <int BPT, int SPS>
+__global__ __launch_bounds__(kS2Threads) void k_score2(ScoreArgs a) {
+  using G = S2Geom<BPT, SPS>;
+  constexpr int P = G::P, H = G::H;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float* tile = reinterpret_cast<float*>(smem);
+  // workgroup -> (slot, band, column tile); slot % 8 == workgroup id % 8 keeps a slot on one XCD
+  const int id = blockIdx.x;
+  const int per = a.n_bands * a.n_ctiles;
+  const int q = id >> 3;
+  const int slot = (q / per) * 8 + (id & 7);
+  if (slot >= a.n_slots) return;
+  const int r = q % per;
+  const int band = r / a.n_ctiles, ct = r - band * a.n_ctiles;
+  const int a0 = a.t0 + band * kS2R;
+  const int c0 = ct * kS2TW;
+  const float* wf = reinterpret_cast<const float*>(a.wf) + (int64_t)slot * a.T * a.F;
+
+  // stage band m: waterfall rows [a0 + 36 m SPS - SPS, + H), columns [c0, c0 + P)
+  for (int i = threadIdx.x; i < G::kFloats; i += kS2Threads) {
+    const int m = i / (H * P), rem = i - m * (H * P);
+    const int rr = rem / P, cc = rem - rr * P;
+    const int row = a0 + 36 * m * SPS - SPS + rr, col = c0 + cc;
+    float v = 0.0f;
+    if (row >= 0 && row < a.T && col < a.F) v = wf[(int64_t)row * a.F + col];
+    tile[i] = v;
+  }
+  __syncthreads();
+
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int af = c0 + 2 * lane;
+  const int nb = a.num_blocks;
+  const int rows = min(kS2R, a.t0 + a.NT - a0);
+  float* out = reinterpret_cast<float*>(a.scores) + (int64_t)slot * a.NT * a.NF;
+  RowSummary* rs = a.rowsum + (int64_t)slot * a.NT;
+  for (int j = w; j < rows; j += kS2Waves) {
+    const int at = a0 + j;                 // wave-uniform
+    const int base = floordiv(at, SPS);
+    f32x2 score = {0.0f, 0.0f};
+    int n = 0;
+    const float* tb = tile + j * P + 2 * lane;
+#pragma unroll
+    for (int m = 0; m < 3; ++m) {
+#pragma unroll
+      for (int k = 0; k < 7; ++k) {
+        const int ba = base + 36 * m + k;
+        if (ba < 0 || ba >= nb) continue;
+        const int tone = kCostasC[k];
+        const float* rp = tb + (m * H + (k + 1) * SPS) * P + tone * BPT;
+        const f32x2 pw = ld2<BPT>(rp);
+        if (tone > 0) { score += pw - ld2<BPT>(rp - BPT); n++; }
+        if (tone < 7) { score += pw - ld2<BPT>(rp + BPT); n++; }
+        if (k > 0 && ba > 0) { score += pw - ld2<BPT>(rp - SPS * P); n++; }
+        if (k < 6 && ba + 1 < nb) { score += pw - ld2<BPT>(rp + SPS * P); n++; }
+      }
+    }
+    float res[2];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const float sc = score[c];
+      res[c] = (n == 0 || isnan(sc) || isinf(sc)) ? -INFINITY : sc / (float)n;
+    }
+    const int ti = at - a.t0;
+    float* orow = out + (int64_t)ti * a.NF;
+    const bool v0 = af < a.NF, v1 = af + 1 < a.NF;
+    if (v0) orow[af] = res[0];
+    if (v1) orow[af + 1] = res[1];
+    const bool p0 = v0 && passes(res[0], a.min_score, a.cmp_f64);
+    const bool p1 = v1 && passes(res[1], a.min_score, a.cmp_f64);
+    const unsigned cnt = (unsigned)(__popcll(__ballot(p0)) + __popcll(__ballot(p1)));
+    if (cnt) {
+      float mx = p0 ? res[0] : -INFINITY;
+      if (p1) mx = fmaxf(mx, res[1]);
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+      if (lane == 0) {
+        atomicAdd(&rs[ti].count, cnt);
+        atomicMax(&rs[ti].maxkey, order_key((double)mx));
+      }
+    }
+  }
+}
+
+template <int BPT, int SPS>
+hipError_t launch_score2(const SyncLaunch& L, const ScoreArgs& a0, hipStream_t s) {
+  using G = S2Geom<BPT, SPS>;
+  ScoreArgs a = a0;
+  a.n_bands = (L.NT + kS2R - 1) / kS2R;
+  a.n_ctiles = (L.NF + kS2TW - 1) / kS2TW;
+  const size_t lds = sizeof(float) * G::kFloats;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_score2<BPT, SPS>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  const int groups = (L.n_slots + 7) / 8;
+  const int64_t blocks = (int64_t)groups * 8 * a.n_bands * a.n_ctiles;
+  hipLaunchKernelGGL((k_score2<BPT, SPS>), dim3((unsigned)blocks), dim3(kS2Threads), lds, s, a);
+  return hipGetLastError();
 }
 
 template <typename T, int TW>
@@ -106,6 +261,23 @@ hipError_t launch_score_t(const SyncLaunch& L, hipStream_t s) {
   a.NT = L.NT;
   a.NF = L.NF;
   a.scores = L.scores;
+  a.rowsum = L.rowsum;
+  a.min_score = L.min_score;
+  a.cmp_f64 = L.min_score_f64;
+  a.n_slots = L.n_slots;
+  hipError_t e = hipMemsetAsync(L.rowsum, 0, sizeof(RowSummary) * (size_t)L.n_slots * L.NT, s);
+  if (e != hipSuccess) return e;
+  if constexpr (sizeof(T) == 4) {
+    if (L.bpt == L.sps) {
+      switch (L.bpt) {
+        case 1: return launch_score2<1, 1>(L, a, s);
+        case 2: return launch_score2<2, 2>(L, a, s);
+        case 3: return launch_score2<3, 3>(L, a, s);
+        case 4: return launch_score2<4, 4>(L, a, s);
+        default: break;
+      }
+    }
+  }
   // rows touched by the grid: [t0 - sps, t0 + NT - 1 + 79 sps], clipped to the waterfall
   a.rlo = max(0, L.t0 - L.sps);
   const int rhi = min(L.T - 1, L.t0 + L.NT - 1 + 79 * L.sps);
@@ -137,6 +309,8 @@ struct SelectArgs {
   int32_t* cand_count;
   int32_t* rec_idx;
   int32_t* warn;
+  const RowSummary* rowsum;
+  int NT;
 };
 
 // block-wide exclusive scans over 1024 threads (int sum and double max), via wave shuffles
@@ -252,6 +426,22 @@ __device__ void bitonic(double* key, int* sec, int* pay, int n) {
 constexpr int kSelV = 4;                        // elements per thread per chunk
 constexpr int kSelChunk = kSelThreads * kSelV;  // 4096 scores per chunk
 
+// block-wide maximum of a u64 key
+__device__ unsigned long long block_max_u64(unsigned long long v, unsigned long long* sh) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long y = __shfl_xor(v, o);
+    v = y > v ? y : v;
+  }
+  if (lane == 0) sh[w] = v;
+  __syncthreads();
+  unsigned long long m = 0;
+  for (int i = 0; i < kSelWaves; ++i) m = sh[i] > m ? sh[i] : m;
+  __syncthreads();
+  return m;
+}
+
 template <typename T>
 __global__ __launch_bounds__(kSelThreads) void k_select(SelectArgs a) {
   __shared__ double s_key[kMaxCandidates + 2];
@@ -260,84 +450,105 @@ __global__ __launch_bounds__(kSelThreads) void k_select(SelectArgs a) {
   __shared__ int s_rank[kMaxCandidates];  // scan index of passing candidate #rank (rank < N)
   __shared__ int s_isum[kSelWaves + 1];
   __shared__ double s_dmax[kSelWaves + 1];
-  __shared__ int s_flag[4];
+  __shared__ unsigned long long s_umax[kSelWaves];
+  __shared__ int s_flag[6];
   __shared__ double s_am_v[kSelWaves];
   __shared__ int s_am_i[kSelWaves];
 
   const int slot = blockIdx.x;
   const T* sc = reinterpret_cast<const T*>(a.scores) + (int64_t)slot * a.total;
+  const RowSummary* rsum = a.rowsum + (int64_t)slot * a.NT;
   int32_t* rec = a.rec_idx + (int64_t)slot * kMaxRecords;
-  const T ms = (T)a.min_score;
-  auto passes = [&](T s) -> bool {
-    if (s == (T)-INFINITY) return false;          // ft8_decode.py:127
-    if (a.cmp_f64) return !((double)s < a.min_score);
-    return !(s < ms);
-  };
   const int N = a.N;
 
-  // one ordered sweep in 4096-score chunks: ranks (exclusive count scan), records (new strict
-  // maxima after rank N, exclusive max scan), first-occurrence argmax (per thread, strict >)
+  // ---- row summaries: total passing, rows holding ranks < N, first row of the global maximum
+  if (threadIdx.x == 0) { s_flag[4] = a.NT; s_flag[5] = a.NT; }
+  int total_pass = 0;
+  unsigned long long gkey = 0;
+  for (int r0 = 0; r0 < a.NT; r0 += kSelThreads) {
+    const int r = r0 + threadIdx.x;
+    const int cnt = r < a.NT ? (int)rsum[r].count : 0;
+    const unsigned long long key = r < a.NT ? rsum[r].maxkey : 0ull;
+    int ctot;
+    const int ex = total_pass + block_excl_sum(cnt, s_isum, &ctot);
+    if (cnt > 0 && ex < N && ex + cnt >= N) s_flag[4] = r + 1;  // exactly one row holds rank N-1
+    const unsigned long long m = block_max_u64(key, s_umax);
+    gkey = m > gkey ? m : gkey;
+    total_pass += ctot;
+  }
+  __syncthreads();
+  if (gkey != 0)
+    for (int r = threadIdx.x; r < a.NT; r += kSelThreads)
+      if (rsum[r].maxkey == gkey) atomicMin(&s_flag[5], r);
+  __syncthreads();
+  const int r_end = s_flag[4];   // rows [0, r_end) hold every rank < N
+  const int g_row = s_flag[5];   // first row holding the global maximum (NT if nothing passes)
+  const double g_val = key_value(gkey);
+  const int nsel = min(total_pass, N);
+
+  // ---- ordered scan of [lo, hi): ranks < N (exclusive count scan), records (strict new maxima
+  // after rank N, exclusive max scan), first-occurrence argmax (per thread, strict >)
   int carry_cnt = 0, carry_rec = 0;
   double carry_max = -INFINITY;
   double best_v = -INFINITY;
   int best_i = 0x7fffffff;
-  for (int64_t c0 = 0; c0 < a.total; c0 += kSelChunk) {
-    T v[kSelV];
-    bool p[kSelV];
-    int lc = 0;
-    double lm = -INFINITY;
-    const int64_t i0 = c0 + (int64_t)threadIdx.x * kSelV;
+  auto scan = [&](int64_t lo, int64_t hi, bool keep_records) {
+    for (int64_t c0 = lo; c0 < hi; c0 += kSelChunk) {
+      T v[kSelV];
+      bool p[kSelV];
+      int lc = 0;
+      double lm = -INFINITY;
+      const int64_t i0 = c0 + (int64_t)threadIdx.x * kSelV;
 #pragma unroll
-    for (int j = 0; j < kSelV; ++j) {
-      const int64_t i = i0 + j;
-      v[j] = i < a.total ? sc[i] : (T)-INFINITY;
-      p[j] = passes(v[j]);
-      if (p[j]) {
-        lc++;
-        lm = fmax(lm, (double)v[j]);
-        if ((double)v[j] > best_v) { best_v = (double)v[j]; best_i = (int)i; }
-      }
-    }
-    int chunk_cnt;
-    double chunk_max;
-    const int ex_cnt = block_excl_sum(lc, s_isum, &chunk_cnt);
-    const double ex_max = block_excl_max(lm, s_dmax, &chunk_max);
-    int rank = carry_cnt + ex_cnt;
-    double rm = fmax(carry_max, ex_max);
-    int nrec = 0;
-    bool isrec[kSelV];
-#pragma unroll
-    for (int j = 0; j < kSelV; ++j) {
-      isrec[j] = false;
-      if (!p[j]) continue;
-      if (rank < N) {
-        s_rank[rank] = (int)(i0 + j);
-      } else if ((double)v[j] > rm) {
-        isrec[j] = true;
-        nrec++;
-      }
-      rm = fmax(rm, (double)v[j]);
-      rank++;
-    }
-    if (__syncthreads_or(nrec > 0)) {
-      int chunk_rec;
-      int r = carry_rec + block_excl_sum(nrec, s_isum, &chunk_rec);
-#pragma unroll
-      for (int j = 0; j < kSelV; ++j)
-        if (isrec[j]) {
-          if (r < kMaxRecords) rec[r] = (int)(i0 + j);
-          r++;
+      for (int j = 0; j < kSelV; ++j) {
+        const int64_t i = i0 + j;
+        v[j] = i < hi ? sc[i] : (T)-INFINITY;
+        p[j] = passes(v[j], a.min_score, a.cmp_f64);
+        if (p[j]) {
+          lc++;
+          lm = fmax(lm, (double)v[j]);
+          if ((double)v[j] > best_v) { best_v = (double)v[j]; best_i = (int)i; }
         }
-      carry_rec += chunk_rec;
+      }
+      int chunk_cnt;
+      double chunk_max;
+      const int ex_cnt = block_excl_sum(lc, s_isum, &chunk_cnt);
+      const double ex_max = block_excl_max(lm, s_dmax, &chunk_max);
+      int rank = carry_cnt + ex_cnt;
+      double rm = fmax(carry_max, ex_max);
+      int nrec = 0;
+      bool isrec[kSelV];
+#pragma unroll
+      for (int j = 0; j < kSelV; ++j) {
+        isrec[j] = false;
+        if (!p[j]) continue;
+        if (rank < N) {
+          s_rank[rank] = (int)(i0 + j);
+        } else if ((double)v[j] > rm) {
+          isrec[j] = true;
+          nrec++;
+        }
+        rm = fmax(rm, (double)v[j]);
+        rank++;
+      }
+      if (__syncthreads_or(nrec > 0)) {
+        int chunk_rec;
+        int r = carry_rec + block_excl_sum(nrec, s_isum, &chunk_rec);
+        if (keep_records) {
+#pragma unroll
+          for (int j = 0; j < kSelV; ++j)
+            if (isrec[j]) {
+              if (r < kMaxRecords) rec[r] = (int)(i0 + j);
+              r++;
+            }
+        }
+        carry_rec += chunk_rec;
+      }
+      carry_cnt += chunk_cnt;
+      carry_max = fmax(carry_max, chunk_max);
     }
-    carry_cnt += chunk_cnt;
-    carry_max = fmax(carry_max, chunk_max);
-  }
-  const int total_pass = carry_cnt, total_rec = carry_rec;
-  const int nsel = min(total_pass, N);
-
-  // first occurrence of the global maximum (the last record, when there are records)
-  {
+  };
+  auto block_argmax = [&]() {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     double bv = best_v;
     int bi = best_i;
@@ -355,12 +566,28 @@ __global__ __launch_bounds__(kSelThreads) void k_select(SelectArgs a) {
           s_am_v[0] = s_am_v[i];
           s_am_i[0] = s_am_i[i];
         }
-      s_flag[0] = 0;
-      s_flag[1] = total_rec > kMaxRecords;
-      s_flag[3] = 0;
+    }
+    __syncthreads();
+  };
+
+  scan(0, (int64_t)r_end * a.NF, false);
+  block_argmax();
+  // a record exists iff the first occurrence of the global maximum has rank >= N; beyond the
+  // scanned rows that is the first passing element of g_row equal to the maximum
+  const bool far = nsel > 0 && g_row >= r_end;
+  if (far) {
+    if (threadIdx.x == 0) s_am_i[0] = 0x7fffffff;
+    __syncthreads();
+    const int64_t base = (int64_t)g_row * a.NF;
+    for (int c = threadIdx.x; c < a.NF; c += kSelThreads) {
+      const T v = sc[base + c];
+      if (passes(v, a.min_score, a.cmp_f64) && (double)v == g_val) atomicMin(&s_am_i[0], (int)(base + c));
     }
     __syncthreads();
   }
+  const bool has_rec = far || carry_rec > 0;
+  if (threadIdx.x == 0) { s_flag[0] = 0; s_flag[1] = 0; s_flag[3] = 0; }
+  __syncthreads();
 
   // the heap keeps the first N; each record evicts the current maximum (the top of the first N,
   // then the previous record): the final set is the first N with its top replaced by the last
@@ -372,7 +599,7 @@ __global__ __launch_bounds__(kSelThreads) void k_select(SelectArgs a) {
     s_pay[i] = idx;
   }
   __syncthreads();
-  if (total_rec > 0 && threadIdx.x == 0) {
+  if (has_rec && threadIdx.x == 0) {
     int top = 0;
     for (int i = 1; i < nsel; ++i)
       if (s_key[i] < s_key[top] || (s_key[i] == s_key[top] && s_sec[i] < s_sec[top])) top = i;
@@ -390,11 +617,40 @@ __global__ __launch_bounds__(kSelThreads) void k_select(SelectArgs a) {
   __syncthreads();
 
   if (s_flag[0]) {
-    // exact score ties in the final set: replay the reference heapq sequence
+    // exact score ties in the final set: collect the records, then replay the reference heapq
+    // sequence.  Records lie in rows [0, r_end) or in a later row whose maximum beats every row
+    // before it; the other rows cannot change the running maximum and are skipped.
+    carry_cnt = 0;
+    carry_rec = 0;
+    carry_max = -INFINITY;
+    scan(0, (int64_t)r_end * a.NF, true);
+    int n_rows = 0;
+    double pmax = -INFINITY;  // maximum over the rows before the current chunk
+    for (int r0 = 0; r0 < a.NT; r0 += kSelThreads) {
+      const int r = r0 + threadIdx.x;
+      const unsigned long long key = r < a.NT ? rsum[r].maxkey : 0ull;
+      const double v = key ? key_value(key) : -INFINITY;
+      double ctot;
+      const double before = fmax(pmax, block_excl_max(v, s_dmax, &ctot));
+      const int want = (r >= r_end && r < a.NT && v > before) ? 1 : 0;
+      int wtot;
+      const int pos = n_rows + block_excl_sum(want, s_isum, &wtot);
+      if (want && pos < kMaxCandidates) s_pay[pos] = r;  // s_pay is free until the final sort
+      n_rows += wtot;
+      pmax = fmax(pmax, ctot);
+    }
+    __syncthreads();
+    for (int i = 0; i < min(n_rows, kMaxCandidates); ++i) {
+      const int64_t lo = (int64_t)s_pay[i] * a.NF;
+      scan(lo, lo + a.NF, true);
+    }
+    if (n_rows > kMaxCandidates) scan((int64_t)(s_pay[kMaxCandidates - 1] + 1) * a.NF, a.total, true);
+    const int total_rec = carry_rec;
     for (int i = threadIdx.x; i < nsel; i += kSelThreads) {
       s_key[i] = -(double)sc[s_rank[i]];
       s_sec[i] = s_rank[i];
     }
+    if (threadIdx.x == 0) s_flag[1] = total_rec > kMaxRecords;
     __syncthreads();
     if (threadIdx.x == 0) {
       HeapCtx h{s_key, s_sec, 0};
@@ -449,6 +705,8 @@ hipError_t launch_select(const SyncLaunch& L, hipStream_t s) {
   a.cand_count = L.cand_count;
   a.rec_idx = L.rec_idx;
   a.warn = L.warn;
+  a.rowsum = L.rowsum;
+  a.NT = max(L.NT, 0);
   if (L.wf_f64)
     hipLaunchKernelGGL(k_select<double>, dim3(L.n_slots), dim3(kSelThreads), 0, s, a);
   else
