@@ -13,6 +13,7 @@ Prints ONE JSON line on rank 0.  Besides the contract fields it carries:
   roofline      the dominant kernel (k_bp: LLR + float64 BP + CRC), FLOP-rate vs the FP64 vector peak
   roofline_hbm  the HBM-bound STFT kernel, GB/s vs the 8 TB/s HBM peak
   stages_ms     per-kernel device time per step (HIP events on the decode stream)
+  bp_stress     BASELINE config 4 first pass: 100k LLR vectors x 50 BP iterations, candidates/s (N=1)
   cpu_baseline  the oracle port (oracle/, C + scipy) on a bounded sample of the same slots (rank 0, N=1)
 """
 import argparse
@@ -75,6 +76,47 @@ def cpu_baseline(kw, n_slots, procs, seed, signals):
             "wall_s": dt}
 
 
+def bp_stress(ctx, dev, n=100000, iters=50, reps=3, sigma=0.85):
+    """BASELINE config 4 (first pass): n LLR vectors from codewords of random payloads,
+    (2b-1) + sigma N(0,1), ftx_normalize_logl on the device, then ft8_bp with `iters` iterations.
+    Returns candidates/s and the k_bp roofline for this launch shape."""
+    import torch
+    from ft8_demodulator_amd import _lib, synth
+    llr, _ = synth.bp_stress_llrs(n, sigma=sigma)
+    a = torch.from_numpy(llr).to(dev)
+    x = torch.empty_like(a)
+    res = torch.zeros(n * _lib.RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+    L, st = _lib.lib(), _lib.stream_handle()
+    ctx.check(L.ft8_normalize(ctx.handle, _lib.ptr(a), n, _lib.ptr(x), st), "ft8_normalize")
+
+    def run():
+        ctx.check(L.ft8_bp(ctx.handle, _lib.ptr(x), n, iters, None, _lib.ptr(res), st), "ft8_bp")
+
+    run()
+    torch.cuda.synchronize()
+    ctx.set_timing(True)
+    ctx.timing(reset=True)
+    ctx.counters(reset=True)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        run()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    ctx.set_timing(False)
+    tm = ctx.timing(reset=True)
+    cn = ctx.counters(reset=True)
+    bp_ms = tm["bp"][0] / max(tm["bp"][1], 1)
+    flops = (cn["passes"] * bp_flops_per_pass() + cn["iterations"] * 174 * 3) / reps
+    tf = flops / (bp_ms * 1e-3) / 1e12
+    return {"workload": f"BASELINE config 4 first pass: {n} LLR vectors (codewords of random payloads, "
+                        f"(2b-1)+{sigma}*N(0,1), normalised), {iters} BP iterations",
+            "candidates_per_s": n * reps / dt, "ms_per_launch": bp_ms,
+            "converged_frac": cn["converged"] / max(cn["candidates"], 1),
+            "sweeps_per_launch": cn["passes"] / reps,
+            "roofline": {"kernel": "k_bp", "bound": "fp64-valu", "achieved": tf, "peak": FP64_VECTOR_PEAK_TFLOPS,
+                         "unit": "TFLOP/s", "frac": tf / FP64_VECTOR_PEAK_TFLOPS}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -84,6 +126,7 @@ def main():
     ap.add_argument("--signals", type=int, default=50)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-slots", type=int, default=256)
+    ap.add_argument("--no-bp-stress", action="store_true", help="skip the config-4 BP stress leg")
     args = ap.parse_args()
 
     import torch
@@ -166,6 +209,10 @@ def main():
     stft_gbs = stft_bytes / (stft_ms * 1e-3) / 1e9
     cand_per_s = cn["candidates"] / K * world / (elapsed / K)
 
+    stress = None
+    if world == 1 and not args.no_bp_stress:
+        stress = bp_stress(ctx, dev)
+
     line = {
         "metric": METRIC,
         "value": value,
@@ -195,6 +242,7 @@ def main():
                          "unit": "GB/s", "frac": stft_gbs / HBM_PEAK_GBS, "traffic": None,
                          "bytes_per_launch": stft_bytes, "launch_ms": stft_ms},
         "stages_ms": stage_ms,
+        "bp_stress": stress,
         "cpu_baseline": cpu,
     }
     if rank == 0:

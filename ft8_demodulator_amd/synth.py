@@ -86,6 +86,46 @@ def random_payload(rng: np.random.Generator) -> bytes:
     return bytes(p)
 
 
+def random_payloads(n: int, rng: np.random.Generator) -> np.ndarray:
+    """[n, 10] uint8 payloads (77 bits, [9] & 0xF8)."""
+    p = rng.integers(0, 256, size=(n, 10), dtype=np.uint8)
+    p[:, 9] &= 0xF8
+    return p
+
+
+def codeword_bits_batch(payloads: np.ndarray) -> np.ndarray:
+    """[n, 10] payloads -> [n, 174] codeword bits (vectorised add_crc + ldpc_encode)."""
+    pay = np.asarray(payloads, dtype=np.uint8).reshape(-1, 10)
+    n = pay.shape[0]
+    a = np.zeros((n, 12), dtype=np.uint8)
+    a[:, :10] = pay
+    a[:, 9] &= 0xF8
+    bits82 = np.unpackbits(a, axis=1)[:, :82].astype(np.int32)
+    rem = np.zeros(n, dtype=np.int32)
+    for i in range(82):  # bitwise CRC-14 (poly 0x2757), MSB first
+        rem ^= bits82[:, i] << 13
+        top = (rem & 0x2000) != 0
+        rem = np.where(top, (rem << 1) ^ 0x2757, rem << 1) & 0x3FFF
+    a[:, 9] |= (rem >> 11).astype(np.uint8)
+    a[:, 10] = ((rem >> 3) & 0xFF).astype(np.uint8)
+    a[:, 11] = ((rem << 5) & 0xE0).astype(np.uint8)
+    msg = np.unpackbits(a, axis=1)[:, :91].astype(np.int32)
+    gen = np.unpackbits(_GEN, axis=1)[:, :91].astype(np.int32)   # [83, 91]
+    parity = (msg @ gen.T) & 1
+    return np.concatenate([msg, parity], axis=1).astype(np.uint8)
+
+
+def bp_stress_llrs(n: int, sigma: float = 0.85, mu: float = 1.0, seed: int = 7):
+    """BASELINE config 4 input: LLRs (2b - 1) mu + sigma N(0, 1) from the
+    codewords of n random payloads (float64 [n, 174], NOT yet normalised) and the bits.  At
+    sigma = 0.85 about half of the vectors fail to converge in 50 iterations after
+    ftx_normalize_logl (oracle: 47 % converge on 1000 vectors)."""
+    rng = np.random.default_rng(seed)
+    bits = codeword_bits_batch(random_payloads(n, rng))
+    llr = (2.0 * bits - 1.0) * mu + sigma * rng.standard_normal(bits.shape)
+    return llr, bits
+
+
 def _pulse(nsps: int, bt: float = 2.0, device=None) -> torch.Tensor:
     k = math.pi * math.sqrt(2.0 / math.log(2.0))
     t = torch.arange(3 * nsps, dtype=torch.float64, device=device) / nsps - 1.5

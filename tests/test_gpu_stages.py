@@ -182,3 +182,22 @@ def test_bp_extreme_inputs_vs_oracle(gpu, oracle):
             pr, er = oracle.bp_decode(llrs[i], it)
             assert er == int(rec[i]["ldpc_errors"]), (it, i)
             assert np.array_equal(pr, p[i]), (it, i)
+
+
+def test_bp_stress_config4_vs_oracle(gpu, oracle):
+    """BASELINE config 4 input (bench.py bp_stress): device-normalised LLRs, 50 iterations; hard
+    decisions, min errors and CRC status bit-exact vs the oracle on 600 vectors."""
+    from ft8_demodulator_amd import _device, synth
+    llr, bits = synth.bp_stress_llrs(600, seed=11)
+    x = _device.normalize(llr)
+    p, rec = _device.bp(x, 50)
+    conv = 0
+    for i in range(600):
+        xr = oracle.normalize(llr[i])
+        assert np.array_equal(x[i].view(np.uint64), xr.view(np.uint64)), i
+        pr, er = oracle.bp_decode(xr, 50)
+        assert er == int(rec[i]["ldpc_errors"]) and np.array_equal(pr, p[i]), i
+        ok, pay, ce, cc = oracle.decode_tail(pr, er)
+        assert bool(rec[i]["ok"]) == ok and int(rec[i]["crc_calculated"]) == cc, i
+        conv += er == 0
+    assert 0.3 < conv / 600 < 0.7   # the ~50 % failure point the workload is defined at

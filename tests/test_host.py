@@ -114,3 +114,13 @@ def test_synth_slot_properties():
         assert p[9] & 0x07 == 0
     y, _ = synth.make_slots(1, 0, seed=4)
     assert abs(float(y.std()) - 1.0) < 0.01
+
+
+def test_codeword_bits_batch_matches_scalar(oracle):
+    from ft8_demodulator_amd import synth
+    rng = np.random.default_rng(9)
+    pay = synth.random_payloads(64, rng)
+    got = synth.codeword_bits_batch(pay)
+    for i in range(64):
+        assert np.array_equal(got[i], synth.codeword_bits(bytes(pay[i])))
+        assert oracle.ldpc_check(got[i]) == 0
