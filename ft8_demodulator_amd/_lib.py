@@ -82,6 +82,7 @@ def lib():
             "ft8_set_timing": ([vp, ctypes.c_int], ctypes.c_int),
             "ft8_get_timing": ([vp, vp, vp, ctypes.c_int], ctypes.c_int),
             "ft8_get_counters": ([vp, vp, ctypes.c_int], ctypes.c_int),
+            "ft8_set_pipeline": ([vp, i32, i32, i32], ctypes.c_int),
         }
         for name, (args, res) in sig.items():
             fn = getattr(L, name)
@@ -95,7 +96,7 @@ def lib():
 EXPORTED_SYMBOLS = (
     "ft8_create", "ft8_destroy", "ft8_last_error", "ft8_abi_version", "ft8_limits", "ft8_geometry",
     "ft8_stft", "ft8_sync_select", "ft8_llr", "ft8_normalize", "ft8_bp", "ft8_decode_batch", "ft8_select_warnings",
-    "ft8_crc14", "ft8_ldpc_check", "ft8_set_timing", "ft8_get_timing", "ft8_get_counters")
+    "ft8_crc14", "ft8_ldpc_check", "ft8_set_timing", "ft8_get_timing", "ft8_get_counters", "ft8_set_pipeline")
 
 
 def limits():
@@ -155,6 +156,11 @@ class Context:
         cnt = (ctypes.c_int64 * N_STAGES)()
         self.check(lib().ft8_get_timing(self.handle, ms, cnt, int(reset)), "ft8_get_timing")
         return {STAGE_NAMES[i]: (ms[i], cnt[i]) for i in range(N_STAGES)}
+
+    def set_pipeline(self, chunk_slots: int = 0, n_streams: int = 0, bp_waves_per_simd: int = 2):
+        """ft8_decode_batch chunking over internal streams (n_streams = 0: one chain)."""
+        self.check(lib().ft8_set_pipeline(self.handle, int(chunk_slots), int(n_streams), int(bp_waves_per_simd)),
+                   "ft8_set_pipeline")
 
     def counters(self, reset: bool = False):
         v = (ctypes.c_int64 * 4)()

@@ -244,6 +244,7 @@ struct BpArgs {
   ft8_result* res;
   unsigned* work;
   unsigned long long* stats;  // nullable: [candidates, iterations entered, message passes, converged]
+  int slot0;
 };
 
 // numpy pairwise sum (loops_utils.h.src) of x[0..174): pw(0,80) + pw(80,94), result in lane 0
@@ -353,6 +354,9 @@ __global__ __launch_bounds__(kWave, BP_WAVES_PER_EU) void k_bp(BpArgs a) {
   if (lane == 0) L.ebits[kEdgeSlots] = 0;
   __syncthreads();
 
+  // work counters, per wave; flushed once when the wave retires (same-address atomics per
+  // candidate would serialise in L2)
+  unsigned st_cand = 0, st_iter = 0, st_pass = 0, st_conv = 0;
   for (;;) {
     unsigned item = 0;
     if (lane == 0) item = atomicAdd(a.work, 1u);
@@ -506,12 +510,10 @@ __global__ __launch_bounds__(kWave, BP_WAVES_PER_EU) void k_bp(BpArgs a) {
       if ((v >> 29) & 1u) L.bits[v & 255] = (uint8_t)((L.ebits[i] >> lane) & 1u);
     }
     __syncthreads();
-    if (a.stats && lane == 0) {
-      atomicAdd(&a.stats[0], 1ull);
-      atomicAdd(&a.stats[1], (unsigned long long)entered);
-      atomicAdd(&a.stats[2], (unsigned long long)passes);
-      if (min_errors == 0) atomicAdd(&a.stats[3], 1ull);
-    }
+    st_cand++;
+    st_iter += entered;
+    st_pass += passes;
+    st_conv += min_errors == 0;
 
     // ---- outputs ------------------------------------------------------------------------------
     if (a.plain_out)
@@ -530,7 +532,7 @@ __global__ __launch_bounds__(kWave, BP_WAVES_PER_EU) void k_bp(BpArgs a) {
       if (lane == 0) {
         ft8_result r;
         r.score = score;
-        r.slot = slot;
+        r.slot = a.slot0 + slot;
         r.abs_time = at;
         r.abs_freq = af;
         r.ldpc_errors = (int16_t)min_errors;
@@ -566,6 +568,12 @@ __global__ __launch_bounds__(kWave, BP_WAVES_PER_EU) void k_bp(BpArgs a) {
       }
     }
     __syncthreads();
+  }
+  if (a.stats && lane == 0 && st_cand) {
+    atomicAdd(&a.stats[0], (unsigned long long)st_cand);
+    atomicAdd(&a.stats[1], (unsigned long long)st_iter);
+    atomicAdd(&a.stats[2], (unsigned long long)st_pass);
+    atomicAdd(&a.stats[3], (unsigned long long)st_conv);
   }
 }
 
@@ -635,6 +643,7 @@ BpArgs make_args(const BpLaunch& L) {
   a.res = L.res;
   a.work = L.work;
   a.stats = L.stats;
+  a.slot0 = L.slot0;
   return a;
 }
 
@@ -655,7 +664,8 @@ hipError_t launch_bp(const BpLaunch& L, hipStream_t s) {
   BpArgs a = make_args(L);
   hipError_t e = hipMemsetAsync(L.work, 0, sizeof(unsigned), s);
   if (e != hipSuccess) return e;
-  const int waves = min(L.n_items, BP_GRID_CUS * 4 * BP_WAVES_PER_EU);  // one resident wave per slot
+  const int per_simd = max(1, min(L.grid_waves, BP_WAVES_PER_EU));
+  const int waves = min(L.n_items, BP_GRID_CUS * 4 * per_simd);  // resident waves, persistent
   hipLaunchKernelGGL(k_bp, dim3(waves), dim3(kWave), 0, s, a);
   return hipGetLastError();
 }

@@ -53,6 +53,12 @@ struct ft8_ctx {
   std::vector<hipEvent_t> pool;
   double ms[FT8_N_STAGES] = {0};
   int64_t launches[FT8_N_STAGES] = {0};
+  // decode_batch pipeline: slot chunks spread over internal streams (0 = one chain on the caller's
+  // stream); BP grid residency in waves per SIMD
+  int chunk_slots = 0, n_streams = 0, bp_waves = 2;
+  std::vector<hipStream_t> streams;
+  hipEvent_t fork = nullptr;
+  std::vector<hipEvent_t> joins;
 };
 
 namespace {
@@ -348,6 +354,10 @@ Grid grid_of(int T, int F, int sps, int bpt) {
   return g;
 }
 
+int sync_select_core(ft8_ctx* c, const void* d_wf, int wf_f64, int n_slots, int T, int F, const ft8_params* p,
+                     int32_t* cand, double* cand_score, int32_t* cand_count, void* scores, int32_t* rec_idx,
+                     int32_t* warn, RowSummary* rowsum, hipStream_t s);
+
 int do_sync_select(ft8_ctx* c, const void* d_wf, int wf_f64, int n_slots, int T, int F, const ft8_params* p,
                    int32_t* cand, double* cand_score, int32_t* cand_count, void* d_scores, hipStream_t s) {
   if (p->steps_per_symbol <= 0 || p->bins_per_tone <= 0) return fail(c, FT8_E_ARG, "bad oversampling factors");
@@ -370,6 +380,17 @@ int do_sync_select(ft8_ctx* c, const void* d_wf, int wf_f64, int n_slots, int T,
   if ((rc = ensure(c, c->rec_idx, sizeof(int32_t) * (size_t)n_slots * kMaxRecords))) return rc;
   if ((rc = ensure(c, c->warn, sizeof(int32_t) * (size_t)n_slots))) return rc;
   if ((rc = ensure(c, c->rowsum, sizeof(RowSummary) * (size_t)n_slots * g.NT))) return rc;
+  return sync_select_core(c, d_wf, wf_f64, n_slots, T, F, p, cand, cand_score, cand_count, scores,
+                          (int32_t*)c->rec_idx.p, (int32_t*)c->warn.p, (RowSummary*)c->rowsum.p, s);
+}
+
+// score + select on caller-provided scratch (scores [n_slots][NT][NF], rec_idx [n_slots][kMaxRecords],
+// warn [n_slots], rowsum [n_slots][NT])
+int sync_select_core(ft8_ctx* c, const void* d_wf, int wf_f64, int n_slots, int T, int F, const ft8_params* p,
+                     int32_t* cand, double* cand_score, int32_t* cand_count, void* scores, int32_t* rec_idx,
+                     int32_t* warn, RowSummary* rowsum, hipStream_t s) {
+  const int N = p->max_candidates;
+  Grid g = grid_of(T, F, p->steps_per_symbol, p->bins_per_tone);
   SyncLaunch L{};
   L.wf = d_wf;
   L.wf_f64 = wf_f64;
@@ -389,9 +410,9 @@ int do_sync_select(ft8_ctx* c, const void* d_wf, int wf_f64, int n_slots, int T,
   L.cand = cand;
   L.cand_score = cand_score;
   L.cand_count = cand_count;
-  L.rec_idx = (int32_t*)c->rec_idx.p;
-  L.warn = (int32_t*)c->warn.p;
-  L.rowsum = (RowSummary*)c->rowsum.p;
+  L.rec_idx = rec_idx;
+  L.warn = warn;
+  L.rowsum = rowsum;
   StageTimer t1(c, 1, s);
   hipError_t e = launch_score(L, s);
   t1.done();
@@ -449,6 +470,9 @@ int ft8_destroy(ft8_ctx* c) {
       (void)hipEventDestroy(t.b);
     }
     for (auto ev : c->pool) (void)hipEventDestroy(ev);
+    for (auto st : c->streams) (void)hipStreamDestroy(st);
+    for (auto ev : c->joins) (void)hipEventDestroy(ev);
+    if (c->fork) (void)hipEventDestroy(c->fork);
   }
   delete c;
   return FT8_OK;
@@ -583,53 +607,109 @@ int ft8_decode_batch(ft8_ctx* c, const void* d_samples, int dtype, int64_t n_sam
   if ((rc = ensure(c, c->cand_count, sizeof(int32_t) * (size_t)n_slots))) return rc;
   if ((rc = ensure(c, c->res_all, sizeof(ft8_result) * (size_t)n_slots * N))) return rc;
   if ((rc = ensure(c, c->llr, sizeof(double) * FT8_LDPC_N * (size_t)n_slots * N))) return rc;
-  if ((rc = ensure(c, c->work, 16))) return rc;
-  if ((rc = do_stft(c, d_samples, dtype, n_samples, n_slots, slot_stride, p, c->wf.p, s))) return rc;
-  if ((rc = do_sync_select(c, c->wf.p, f64, n_slots, T, F, p, (int32_t*)c->cand.p, (double*)c->cand_score.p,
-                           (int32_t*)c->cand_count.p, nullptr, s)))
-    return rc;
-  BpLaunch B{};
-  B.wf = c->wf.p;
-  B.wf_f64 = f64;
-  B.T = T;
-  B.F = F;
-  B.sps = p->steps_per_symbol;
-  B.bpt = p->bins_per_tone;
-  B.cand = (const int32_t*)c->cand.p;
-  B.cand_score = (const double*)c->cand_score.p;
-  B.cand_count = (const int32_t*)c->cand_count.p;
-  B.N = N;
-  B.n_slots = n_slots;
-  B.n_items = n_slots * N;
-  B.mode = 0;
-  B.normalize = 1;
-  B.max_iterations = p->max_iterations;
-  B.llr_out = (double*)c->llr.p;
-  B.llr_in = (const double*)c->llr.p;
-  B.res = (ft8_result*)c->res_all.p;
-  B.work = (unsigned*)c->work.p;
-  B.stats = (unsigned long long*)c->stats.p;
-  StageTimer t6(c, 6, s);
-  hipError_t e = launch_llr(B, s);
-  t6.done();
-  if (e != hipSuccess) return hipfail(c, e, "llr launch");
-  StageTimer t3(c, 3, s);
-  e = launch_bp(B, s);
-  t3.done();
-  if (e != hipSuccess) return hipfail(c, e, "bp launch");
-  CompactLaunch C{};
-  C.res = (const ft8_result*)c->res_all.p;
-  C.cand_count = (const int32_t*)c->cand_count.p;
-  C.n_slots = n_slots;
-  C.N = N;
-  C.out = d_out;
-  C.counts = d_counts;
-  C.cap = cap;
-  StageTimer t4(c, 4, s);
-  e = launch_compact(C, s);
-  t4.done();
+  if ((rc = ensure(c, c->scores, esz * (size_t)n_slots * gr.NT * gr.NF))) return rc;
+  if ((rc = ensure(c, c->rec_idx, sizeof(int32_t) * (size_t)n_slots * kMaxRecords))) return rc;
+  if ((rc = ensure(c, c->warn, sizeof(int32_t) * (size_t)n_slots))) return rc;
+  if ((rc = ensure(c, c->rowsum, sizeof(RowSummary) * (size_t)n_slots * gr.NT))) return rc;
+  if (p->steps_per_symbol <= 0 || p->bins_per_tone <= 0) return fail(c, FT8_E_ARG, "bad oversampling factors");
+  if (p->flags & FT8_FLAG_TOPK) return fail(c, FT8_E_UNSUPPORTED, "FT8_FLAG_TOPK is not implemented yet");
+
+  // slot chunks, each an independent STFT -> score/select -> LLR -> BP -> compact chain; chunks
+  // alternate over the internal streams so one chunk's BP (FP64 VALU) overlaps the next chunk's
+  // STFT / score (LDS, HBM)
+  const int csz = (c->n_streams > 0 && c->chunk_slots > 0) ? c->chunk_slots : n_slots;
+  const int n_chunks = (n_slots + csz - 1) / csz;
+  const int n_str = (c->n_streams > 0 && n_chunks > 1) ? std::min(c->n_streams, n_chunks) : 0;
+  if ((rc = ensure(c, c->work, sizeof(unsigned) * (size_t)std::max(n_chunks, 4)))) return rc;
+  hipError_t e = hipSuccess;
+  if (n_str > 0) {
+    while ((int)c->streams.size() < n_str) {
+      hipStream_t st;
+      if ((e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking)) != hipSuccess) return hipfail(c, e, "stream");
+      c->streams.push_back(st);
+      hipEvent_t ev;
+      if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return hipfail(c, e, "event");
+      c->joins.push_back(ev);
+    }
+    if (!c->fork && (e = hipEventCreateWithFlags(&c->fork, hipEventDisableTiming)) != hipSuccess)
+      return hipfail(c, e, "event");
+    if ((e = hipEventRecord(c->fork, s)) != hipSuccess) return hipfail(c, e, "fork");
+    for (int i = 0; i < n_str; ++i)
+      if ((e = hipStreamWaitEvent(c->streams[i], c->fork, 0)) != hipSuccess) return hipfail(c, e, "fork wait");
+  }
+  const size_t in_esz = dtype == FT8_I16 ? 2 : dtype == FT8_F32 ? 4 : (dtype == FT8_F64 || dtype == FT8_C64) ? 8 : 16;
+  for (int k = 0; k < n_chunks; ++k) {
+    const int c0 = k * csz, ns = std::min(csz, n_slots - c0);
+    hipStream_t cs = n_str > 0 ? c->streams[k % n_str] : s;
+    char* wf = (char*)c->wf.p + esz * (size_t)c0 * T * F;
+    const char* xs = (const char*)d_samples + in_esz * (size_t)c0 * slot_stride;
+    if ((rc = do_stft(c, xs, dtype, n_samples, ns, slot_stride, p, wf, cs))) return rc;
+    int32_t* cand = (int32_t*)c->cand.p + 2 * (size_t)c0 * N;
+    double* cand_score = (double*)c->cand_score.p + (size_t)c0 * N;
+    int32_t* cand_count = (int32_t*)c->cand_count.p + c0;
+    if ((rc = sync_select_core(c, wf, f64, ns, T, F, p, cand, cand_score, cand_count,
+                               (char*)c->scores.p + esz * (size_t)c0 * gr.NT * gr.NF,
+                               (int32_t*)c->rec_idx.p + (size_t)c0 * kMaxRecords, (int32_t*)c->warn.p + c0,
+                               (RowSummary*)c->rowsum.p + (size_t)c0 * gr.NT, cs)))
+      return rc;
+    BpLaunch B{};
+    B.wf = wf;
+    B.wf_f64 = f64;
+    B.T = T;
+    B.F = F;
+    B.sps = p->steps_per_symbol;
+    B.bpt = p->bins_per_tone;
+    B.cand = cand;
+    B.cand_score = cand_score;
+    B.cand_count = cand_count;
+    B.N = N;
+    B.n_slots = ns;
+    B.slot0 = c0;
+    B.n_items = ns * N;
+    B.mode = 0;
+    B.normalize = 1;
+    B.max_iterations = p->max_iterations;
+    B.llr_out = (double*)c->llr.p + (size_t)FT8_LDPC_N * c0 * N;
+    B.llr_in = B.llr_out;
+    B.res = (ft8_result*)c->res_all.p + (size_t)c0 * N;
+    B.work = (unsigned*)c->work.p + k;
+    B.stats = (unsigned long long*)c->stats.p;
+    B.grid_waves = n_str > 0 ? c->bp_waves : 4;
+    StageTimer t6(c, 6, cs);
+    e = launch_llr(B, cs);
+    t6.done();
+    if (e != hipSuccess) return hipfail(c, e, "llr launch");
+    StageTimer t3(c, 3, cs);
+    e = launch_bp(B, cs);
+    t3.done();
+    if (e != hipSuccess) return hipfail(c, e, "bp launch");
+    CompactLaunch C{};
+    C.res = B.res;
+    C.cand_count = cand_count;
+    C.n_slots = ns;
+    C.N = N;
+    C.out = d_out ? d_out + (size_t)c0 * cap : nullptr;
+    C.counts = d_counts + c0;
+    C.cap = cap;
+    StageTimer t4(c, 4, cs);
+    e = launch_compact(C, cs);
+    t4.done();
+    if (e != hipSuccess) return hipfail(c, e, "compact launch");
+  }
+  for (int i = 0; i < n_str; ++i) {
+    if ((e = hipEventRecord(c->joins[i], c->streams[i])) != hipSuccess) return hipfail(c, e, "join");
+    if ((e = hipStreamWaitEvent(s, c->joins[i], 0)) != hipSuccess) return hipfail(c, e, "join wait");
+  }
   whole.done();
-  if (e != hipSuccess) return hipfail(c, e, "compact launch");
+  return FT8_OK;
+}
+
+int ft8_set_pipeline(ft8_ctx* c, int32_t chunk_slots, int32_t n_streams, int32_t bp_waves_per_simd) {
+  if (!c || chunk_slots < 0 || n_streams < 0 || n_streams > 8 || bp_waves_per_simd < 1 || bp_waves_per_simd > 4)
+    return fail(c, FT8_E_ARG, "bad pipeline setting");
+  c->chunk_slots = chunk_slots;
+  c->n_streams = n_streams;
+  c->bp_waves = bp_waves_per_simd;
   return FT8_OK;
 }
 

@@ -110,6 +110,8 @@ struct BpLaunch {
   ft8_result* res;         // nullable [n_items]
   unsigned* work;          // work counter (zeroed by the launcher)
   unsigned long long* stats = nullptr;  // [candidates, iterations entered, message passes, converged]
+  int slot0 = 0;           // batch index of slot 0 (records carry slot0 + local slot)
+  int grid_waves = 4;      // k_bp persistent grid: resident waves per SIMD (<= BP_WAVES_PER_EU)
 };
 hipError_t launch_llr(const BpLaunch& a, hipStream_t s);  // k_llr: waterfall -> LLRs
 hipError_t launch_bp(const BpLaunch& a, hipStream_t s);   // k_bp: LLRs -> BP + CRC

@@ -107,3 +107,21 @@ def test_stft_i16_equals_f32(gpu):
     ctx.check(_lib.lib().ft8_stft(ctx.handle, _lib.ptr(xi), _lib.FT8_I16, len(raw), 1, len(raw), ctypes.byref(p),
                                   _lib.ptr(out), _lib.stream_handle()), "stft")
     assert torch.equal(out, a)
+
+
+def test_pipeline_settings_do_not_change_results(gpu):
+    """ft8_decode_batch cut into slot chunks over internal streams returns the same records as one
+    chain on the caller's stream."""
+    from ft8_demodulator_amd import SlotDecoder, synth
+    x, _ = synth.make_slots(40, 30, seed=4242, device="cuda")
+    dec = SlotDecoder(12000, 2, 2, 100, 3, 20)
+    got = {}
+    for cfg in [(0, 0, 4), (8, 2, 2), (16, 3, 1), (7, 2, 4)]:
+        dec.ctx.set_pipeline(*cfg)
+        out, cnt = dec.run(x)
+        got[cfg] = (out.cpu().numpy().tobytes(), cnt.cpu().numpy().tobytes())
+    dec.ctx.set_pipeline()
+    base = got[(0, 0, 4)]
+    assert sum(np.frombuffer(base[1], np.int32)) > 0
+    for cfg, v in got.items():
+        assert v == base, cfg
