@@ -47,7 +47,7 @@ struct ft8_ctx {
   std::string err;
   std::vector<PlanEntry> plans;
   std::vector<WinEntry> wins;
-  DevBuf wf, scores, cand, cand_score, cand_count, rec_idx, warn, rowsum, res_all, work, stats, llr;
+  DevBuf wf, scores, cand, cand_score, cand_count, warn, rowsum, res_all, work, stats, llr;
   bool timing = false;
   std::vector<TimedLaunch> pending;
   std::vector<hipEvent_t> pool;
@@ -355,7 +355,7 @@ Grid grid_of(int T, int F, int sps, int bpt) {
 }
 
 int sync_select_core(ft8_ctx* c, const void* d_wf, int wf_f64, int n_slots, int T, int F, const ft8_params* p,
-                     int32_t* cand, double* cand_score, int32_t* cand_count, void* scores, int32_t* rec_idx,
+                     int32_t* cand, double* cand_score, int32_t* cand_count, void* scores,
                      int32_t* warn, RowSummary* rowsum, hipStream_t s);
 
 int do_sync_select(ft8_ctx* c, const void* d_wf, int wf_f64, int n_slots, int T, int F, const ft8_params* p,
@@ -377,17 +377,16 @@ int do_sync_select(ft8_ctx* c, const void* d_wf, int wf_f64, int n_slots, int T,
     if ((rc = ensure(c, c->scores, esz * (size_t)n_slots * g.NT * g.NF))) return rc;
     scores = c->scores.p;
   }
-  if ((rc = ensure(c, c->rec_idx, sizeof(int32_t) * (size_t)n_slots * kMaxRecords))) return rc;
   if ((rc = ensure(c, c->warn, sizeof(int32_t) * (size_t)n_slots))) return rc;
   if ((rc = ensure(c, c->rowsum, sizeof(RowSummary) * (size_t)n_slots * g.NT))) return rc;
   return sync_select_core(c, d_wf, wf_f64, n_slots, T, F, p, cand, cand_score, cand_count, scores,
-                          (int32_t*)c->rec_idx.p, (int32_t*)c->warn.p, (RowSummary*)c->rowsum.p, s);
+                          (int32_t*)c->warn.p, (RowSummary*)c->rowsum.p, s);
 }
 
-// score + select on caller-provided scratch (scores [n_slots][NT][NF], rec_idx [n_slots][kMaxRecords],
-// warn [n_slots], rowsum [n_slots][NT])
+// score + select on caller-provided scratch (scores [n_slots][NT][NF], warn [n_slots],
+// rowsum [n_slots][NT])
 int sync_select_core(ft8_ctx* c, const void* d_wf, int wf_f64, int n_slots, int T, int F, const ft8_params* p,
-                     int32_t* cand, double* cand_score, int32_t* cand_count, void* scores, int32_t* rec_idx,
+                     int32_t* cand, double* cand_score, int32_t* cand_count, void* scores,
                      int32_t* warn, RowSummary* rowsum, hipStream_t s) {
   const int N = p->max_candidates;
   Grid g = grid_of(T, F, p->steps_per_symbol, p->bins_per_tone);
@@ -410,7 +409,6 @@ int sync_select_core(ft8_ctx* c, const void* d_wf, int wf_f64, int n_slots, int 
   L.cand = cand;
   L.cand_score = cand_score;
   L.cand_count = cand_count;
-  L.rec_idx = rec_idx;
   L.warn = warn;
   L.rowsum = rowsum;
   StageTimer t1(c, 1, s);
@@ -456,7 +454,7 @@ int ft8_destroy(ft8_ctx* c) {
   if (!c) return FT8_OK;
   {
     DeviceGuard dg(c->device);
-    for (auto* b : {&c->wf, &c->scores, &c->cand, &c->cand_score, &c->cand_count, &c->rec_idx, &c->warn, &c->rowsum,
+    for (auto* b : {&c->wf, &c->scores, &c->cand, &c->cand_score, &c->cand_count, &c->warn, &c->rowsum,
                     &c->res_all, &c->work, &c->stats, &c->llr})
       if (b->p) (void)hipFree(b->p);
     for (auto& p : c->plans) {
@@ -608,7 +606,6 @@ int ft8_decode_batch(ft8_ctx* c, const void* d_samples, int dtype, int64_t n_sam
   if ((rc = ensure(c, c->res_all, sizeof(ft8_result) * (size_t)n_slots * N))) return rc;
   if ((rc = ensure(c, c->llr, sizeof(double) * FT8_LDPC_N * (size_t)n_slots * N))) return rc;
   if ((rc = ensure(c, c->scores, esz * (size_t)n_slots * gr.NT * gr.NF))) return rc;
-  if ((rc = ensure(c, c->rec_idx, sizeof(int32_t) * (size_t)n_slots * kMaxRecords))) return rc;
   if ((rc = ensure(c, c->warn, sizeof(int32_t) * (size_t)n_slots))) return rc;
   if ((rc = ensure(c, c->rowsum, sizeof(RowSummary) * (size_t)n_slots * gr.NT))) return rc;
   if (p->steps_per_symbol <= 0 || p->bins_per_tone <= 0) return fail(c, FT8_E_ARG, "bad oversampling factors");
@@ -648,8 +645,7 @@ int ft8_decode_batch(ft8_ctx* c, const void* d_samples, int dtype, int64_t n_sam
     double* cand_score = (double*)c->cand_score.p + (size_t)c0 * N;
     int32_t* cand_count = (int32_t*)c->cand_count.p + c0;
     if ((rc = sync_select_core(c, wf, f64, ns, T, F, p, cand, cand_score, cand_count,
-                               (char*)c->scores.p + esz * (size_t)c0 * gr.NT * gr.NF,
-                               (int32_t*)c->rec_idx.p + (size_t)c0 * kMaxRecords, (int32_t*)c->warn.p + c0,
+                               (char*)c->scores.p + esz * (size_t)c0 * gr.NT * gr.NF, (int32_t*)c->warn.p + c0,
                                (RowSummary*)c->rowsum.p + (size_t)c0 * gr.NT, cs)))
       return rc;
     BpLaunch B{};

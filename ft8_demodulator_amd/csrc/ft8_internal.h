@@ -13,7 +13,6 @@ constexpr int kWave = 64;
 constexpr int kMaxCandidates = 4096;   // LDS-resident selection (k_select)
 constexpr int kMaxFftReal = 16384;     // nfft of the real-input path (half-length FFT <= 8192)
 constexpr int kMaxFftComplex = 8192;   // nfft of the complex-input path
-constexpr int kMaxRecords = 2048;      // new-maximum records kept per slot for the exact heap replay
 
 __host__ __device__ inline int floordiv(int a, int b) {
   int q = a / b;
@@ -81,9 +80,8 @@ struct SyncLaunch {
   int32_t* cand;           // [n_slots][N][2]
   double* cand_score;      // [n_slots][N]
   int32_t* cand_count;     // [n_slots]
-  int32_t* rec_idx;        // scratch [n_slots][kMaxRecords]
   int32_t* warn;           // scratch [n_slots] (bit 0: tie reached a heap comparison,
-                           //                    bit 1: record overflow -> approximate tie order)
+                           //                    bit 2: equal scores in the selected set)
   RowSummary* rowsum;      // scratch [n_slots][NT]: passing count + max passing score per time row
 };
 hipError_t launch_score(const SyncLaunch& a, hipStream_t s);

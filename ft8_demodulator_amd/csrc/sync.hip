@@ -29,8 +29,8 @@
 // first occurrence of the global maximum when that lies beyond rank N.  From the row summaries
 // the kernel finds the rows holding ranks < N and the row of the global maximum, and scans only
 // those; it sorts the set by score, and only when two selected scores are exactly equal (where
-// the reference's order depends on heap array positions) rescans the whole grid for the records
-// and replays the reference heapq sequence in LDS to reproduce its stable sort.
+// the reference's order depends on heap array positions) replays the reference's N heappushes
+// (one wave wide) to rebuild the heap array and reproduce its stable sort.
 #include "ft8_internal.h"
 
 namespace ft8 {
@@ -307,7 +307,6 @@ struct SelectArgs {
   int32_t* cand;
   double* cand_score;
   int32_t* cand_count;
-  int32_t* rec_idx;
   int32_t* warn;
   const RowSummary* rowsum;
   int NT;
@@ -357,45 +356,6 @@ __device__ double block_excl_max(double v, double* sh, double* total) {
   *total = sh[kSelWaves];
   __syncthreads();
   return r;
-}
-
-// heap key: (neg score, secondary); equal neg => tie (the reference would compare candidates)
-struct HeapCtx {
-  double* neg;
-  int* idx;
-  int tie;
-  __device__ bool less(int a, int b) {
-    if (neg[a] < neg[b]) return true;
-    if (neg[a] > neg[b]) return false;
-    tie = 1;
-    return idx[a] < idx[b];
-  }
-  __device__ void mov(int dst, int src) { neg[dst] = neg[src]; idx[dst] = idx[src]; }
-};
-
-// CPython heapq _siftdown / _siftup on LDS arrays; slot `tmp` (= capacity) holds newitem
-__device__ void h_siftdown(HeapCtx& h, int start, int pos, int tmp) {
-  h.mov(tmp, pos);
-  while (pos > start) {
-    const int pp = (pos - 1) >> 1;
-    if (h.less(tmp, pp)) { h.mov(pos, pp); pos = pp; continue; }
-    break;
-  }
-  h.mov(pos, tmp);
-}
-__device__ void h_siftup(HeapCtx& h, int len, int pos, int tmp) {
-  const int start = pos;
-  h.mov(tmp + 1, pos);  // newitem
-  int c = 2 * pos + 1;
-  while (c < len) {
-    const int r = c + 1;
-    if (r < len && !h.less(c, r)) c = r;
-    h.mov(pos, c);
-    pos = c;
-    c = 2 * pos + 1;
-  }
-  h.mov(pos, tmp + 1);
-  h_siftdown(h, start, pos, tmp);
 }
 
 // bitonic sort of n items by (key asc, sec asc) in LDS (padded to a power of two <= cap)
@@ -458,7 +418,6 @@ __global__ __launch_bounds__(kSelThreads) void k_select(SelectArgs a) {
   const int slot = blockIdx.x;
   const T* sc = reinterpret_cast<const T*>(a.scores) + (int64_t)slot * a.total;
   const RowSummary* rsum = a.rowsum + (int64_t)slot * a.NT;
-  int32_t* rec = a.rec_idx + (int64_t)slot * kMaxRecords;
   const int N = a.N;
 
   // ---- row summaries: total passing, rows holding ranks < N, first row of the global maximum
@@ -492,7 +451,7 @@ __global__ __launch_bounds__(kSelThreads) void k_select(SelectArgs a) {
   double carry_max = -INFINITY;
   double best_v = -INFINITY;
   int best_i = 0x7fffffff;
-  auto scan = [&](int64_t lo, int64_t hi, bool keep_records) {
+  auto scan = [&](int64_t lo, int64_t hi) {
     for (int64_t c0 = lo; c0 < hi; c0 += kSelChunk) {
       T v[kSelV];
       bool p[kSelV];
@@ -517,33 +476,18 @@ __global__ __launch_bounds__(kSelThreads) void k_select(SelectArgs a) {
       int rank = carry_cnt + ex_cnt;
       double rm = fmax(carry_max, ex_max);
       int nrec = 0;
-      bool isrec[kSelV];
 #pragma unroll
       for (int j = 0; j < kSelV; ++j) {
-        isrec[j] = false;
         if (!p[j]) continue;
         if (rank < N) {
           s_rank[rank] = (int)(i0 + j);
         } else if ((double)v[j] > rm) {
-          isrec[j] = true;
           nrec++;
         }
         rm = fmax(rm, (double)v[j]);
         rank++;
       }
-      if (__syncthreads_or(nrec > 0)) {
-        int chunk_rec;
-        int r = carry_rec + block_excl_sum(nrec, s_isum, &chunk_rec);
-        if (keep_records) {
-#pragma unroll
-          for (int j = 0; j < kSelV; ++j)
-            if (isrec[j]) {
-              if (r < kMaxRecords) rec[r] = (int)(i0 + j);
-              r++;
-            }
-        }
-        carry_rec += chunk_rec;
-      }
+      if (__syncthreads_or(nrec > 0)) carry_rec++;  // only "any record" matters
       carry_cnt += chunk_cnt;
       carry_max = fmax(carry_max, chunk_max);
     }
@@ -570,7 +514,7 @@ __global__ __launch_bounds__(kSelThreads) void k_select(SelectArgs a) {
     __syncthreads();
   };
 
-  scan(0, (int64_t)r_end * a.NF, false);
+  scan(0, (int64_t)r_end * a.NF);
   block_argmax();
   // a record exists iff the first occurrence of the global maximum has rank >= N; beyond the
   // scanned rows that is the first passing element of g_row equal to the maximum
@@ -599,14 +543,50 @@ __global__ __launch_bounds__(kSelThreads) void k_select(SelectArgs a) {
     s_pay[i] = idx;
   }
   __syncthreads();
-  if (has_rec && threadIdx.x == 0) {
-    int top = 0;
-    for (int i = 1; i < nsel; ++i)
-      if (s_key[i] < s_key[top] || (s_key[i] == s_key[top] && s_sec[i] < s_sec[top])) top = i;
-    const int gi = s_am_i[0];
-    s_key[top] = -(double)sc[gi];
-    s_sec[top] = gi;
-    s_pay[top] = gi;
+  if (has_rec) {
+    // the top of the first N (largest score, first in scan order among equals) is evicted; if its
+    // score occurs twice among the first N the reference heap may have compared the two (tie)
+    int top = 0x7fffffff;
+    double tk = INFINITY;
+    for (int i = threadIdx.x; i < nsel; i += kSelThreads)
+      if (s_key[i] < tk || (s_key[i] == tk && s_sec[i] < s_sec[top])) { tk = s_key[i]; top = i; }
+    {
+      const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const double ok = __shfl_xor(tk, o);
+        const int ot = __shfl_xor(top, o);
+        const bool better = ot != 0x7fffffff &&
+                            (top == 0x7fffffff || ok < tk || (ok == tk && s_sec[ot] < s_sec[top]));
+        if (better) { tk = ok; top = ot; }
+      }
+      if (lane == 0) { s_am_v[w] = tk; s_isum[w] = top; }
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        for (int i = 1; i < kSelWaves; ++i) {
+          const int ot = s_isum[i];
+          if (ot == 0x7fffffff) continue;
+          if (top == 0x7fffffff || s_am_v[i] < tk || (s_am_v[i] == tk && s_sec[ot] < s_sec[top])) {
+            tk = s_am_v[i];
+            top = ot;
+          }
+        }
+        s_isum[0] = top;
+        s_am_v[0] = tk;
+      }
+      __syncthreads();
+      top = s_isum[0];
+      tk = s_am_v[0];
+    }
+    for (int i = threadIdx.x; i < nsel; i += kSelThreads)
+      if (i != top && s_key[i] == tk) s_flag[0] = 1;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const int gi = s_am_i[0];
+      s_key[top] = -(double)sc[gi];
+      s_sec[top] = gi;
+      s_pay[top] = gi;
+    }
   }
   __syncthreads();
 
@@ -617,52 +597,63 @@ __global__ __launch_bounds__(kSelThreads) void k_select(SelectArgs a) {
   __syncthreads();
 
   if (s_flag[0]) {
-    // exact score ties in the final set: collect the records, then replay the reference heapq
-    // sequence.  Records lie in rows [0, r_end) or in a later row whose maximum beats every row
-    // before it; the other rows cannot change the running maximum and are skipped.
-    carry_cnt = 0;
-    carry_rec = 0;
-    carry_max = -INFINITY;
-    scan(0, (int64_t)r_end * a.NF, true);
-    int n_rows = 0;
-    double pmax = -INFINITY;  // maximum over the rows before the current chunk
-    for (int r0 = 0; r0 < a.NT; r0 += kSelThreads) {
-      const int r = r0 + threadIdx.x;
-      const unsigned long long key = r < a.NT ? rsum[r].maxkey : 0ull;
-      const double v = key ? key_value(key) : -INFINITY;
-      double ctot;
-      const double before = fmax(pmax, block_excl_max(v, s_dmax, &ctot));
-      const int want = (r >= r_end && r < a.NT && v > before) ? 1 : 0;
-      int wtot;
-      const int pos = n_rows + block_excl_sum(want, s_isum, &wtot);
-      if (want && pos < kMaxCandidates) s_pay[pos] = r;  // s_pay is free until the final sort
-      n_rows += wtot;
-      pmax = fmax(pmax, ctot);
-    }
-    __syncthreads();
-    for (int i = 0; i < min(n_rows, kMaxCandidates); ++i) {
-      const int64_t lo = (int64_t)s_pay[i] * a.NF;
-      scan(lo, lo + a.NF, true);
-    }
-    if (n_rows > kMaxCandidates) scan((int64_t)(s_pay[kMaxCandidates - 1] + 1) * a.NF, a.total, true);
-    const int total_rec = carry_rec;
+    // Exact score ties in the final set: their order is the reference heap's array order, so
+    // rebuild that array.  heapreplace of a record (a strict new maximum, ft8_decode.py:134-137)
+    // moves the min-child path up and sifts the record back to the root, which restores every
+    // other position: the final heap is the heap of the first N pushes with its root replaced by
+    // the last record.  Only the N heappushes need replaying, one wave wide: lane j holds the
+    // j-th ancestor of the new position, a ballot finds how far the item rises.
     for (int i = threadIdx.x; i < nsel; i += kSelThreads) {
       s_key[i] = -(double)sc[s_rank[i]];
       s_sec[i] = s_rank[i];
     }
-    if (threadIdx.x == 0) s_flag[1] = total_rec > kMaxRecords;
     __syncthreads();
-    if (threadIdx.x == 0) {
-      HeapCtx h{s_key, s_sec, 0};
-      for (int n = 1; n < nsel; ++n) h_siftdown(h, 0, n, kMaxCandidates);  // heappush x nsel
-      const int nr = min(total_rec, kMaxRecords);
-      for (int r = 0; r < nr; ++r) {  // heapreplace(heap, record)
-        const int i = rec[r];
-        s_key[0] = -(double)sc[i];
-        s_sec[0] = i;
-        h_siftup(h, nsel, 0, kMaxCandidates);
+    if (threadIdx.x < kWave) {
+      const int lane = threadIdx.x;
+      int tie = 0;
+      for (int n = 1; n < nsel; ++n) {
+        const double nk = s_key[n];
+        const int ni = s_sec[n];
+        const int d = 31 - __clz(n + 1);  // ancestors of position n
+        double ak = 0.0;
+        int ai = 0;
+        if (lane < d) {
+          const int pj = ((n + 1) >> (lane + 1)) - 1;
+          ak = s_key[pj];
+          ai = s_sec[pj];
+        }
+        const bool lt = lane < d && (nk < ak || (nk == ak && ni < ai));
+        const int m = __ffsll((long long)~__ballot(lt)) - 1;  // the item passes ancestors 0..m-1
+        if (__any(lane < d && lane <= m && nk == ak)) tie = 1;  // a compared parent with an equal key
+        if (lane < m) {
+          const int dest = lane == 0 ? n : ((n + 1) >> lane) - 1;
+          s_key[dest] = ak;
+          s_sec[dest] = ai;
+        }
+        if (lane == 0) {
+          const int dest = m == 0 ? n : ((n + 1) >> m) - 1;
+          s_key[dest] = nk;
+          s_sec[dest] = ni;
+        }
+        asm volatile("" ::: "memory");  // the next push reads what this one wrote (in-order LDS)
       }
-      s_flag[3] = h.tie;
+      if (lane == 0 && has_rec) {
+        // the records' _siftup compares siblings along the min-child path (same path each time)
+        int c = 1;
+        while (c < nsel) {
+          const int r = c + 1;
+          if (r < nsel) {
+            if (s_key[c] == s_key[r]) tie = 1;
+            const bool cl = s_key[c] < s_key[r] || (s_key[c] == s_key[r] && s_sec[c] < s_sec[r]);
+            if (!cl) c = r;
+          }
+          c = 2 * c + 1;
+        }
+        const int gi = s_am_i[0];
+        s_key[0] = -(double)sc[gi];
+        s_sec[0] = gi;
+      }
+      if (lane == 0) s_flag[3] = tie;
     }
     __syncthreads();
     // sorted(key=-score) is stable on heap-array order: secondary key = heap position
@@ -672,7 +663,7 @@ __global__ __launch_bounds__(kSelThreads) void k_select(SelectArgs a) {
   }
   if (threadIdx.x == 0) {
     a.cand_count[slot] = nsel;
-    a.warn[slot] = (s_flag[3] ? 1 : 0) | (s_flag[1] && s_flag[0] ? 2 : 0);
+    a.warn[slot] = (s_flag[3] ? 1 : 0) | (s_flag[0] ? 4 : 0);
   }
   for (int i = threadIdx.x; i < nsel; i += kSelThreads) {
     const int idx = s_pay[i];
@@ -703,7 +694,6 @@ hipError_t launch_select(const SyncLaunch& L, hipStream_t s) {
   a.cand = L.cand;
   a.cand_score = L.cand_score;
   a.cand_count = L.cand_count;
-  a.rec_idx = L.rec_idx;
   a.warn = L.warn;
   a.rowsum = L.rowsum;
   a.NT = max(L.NT, 0);

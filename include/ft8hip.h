@@ -85,7 +85,7 @@ int ft8_create(int device, ft8_ctx** out);
 int ft8_destroy(ft8_ctx* ctx);
 const char* ft8_last_error(const ft8_ctx* ctx);
 int ft8_abi_version(void);
-/* compiled limits: max_candidates, max FFT length (real / complex), max records per slot */
+/* compiled limits: max_candidates, max FFT length (real / complex) */
 int ft8_limits(int32_t* max_candidates, int32_t* max_fft_real, int32_t* max_fft_complex);
 
 /* STFT geometry of calculate_spectrogram (spectrogram_analyse.py:31-43): window length,
@@ -154,8 +154,9 @@ int ft8_set_pipeline(ft8_ctx* ctx, int32_t chunk_slots, int32_t n_streams, int32
 
 /* Per-slot flags of the last selection (copied device->device into d_out[n_slots]):
  * bit 0: an exact score tie reached a heap comparison (the reference raises TypeError there,
- *        ftx_types.py:37-47; here ties are ordered by scan index), bit 1: more new-maximum records
- *        than kept, tie order approximate. */
+ *        ftx_types.py:37-47; here ties are ordered by scan index), bit 1: unused (0), bit 2
+ *        (informational): the selected set held equal scores, so the heap sequence was replayed
+ *        to order them. */
 int ft8_select_warnings(ft8_ctx* ctx, int32_t* d_out, int32_t n_slots, void* stream);
 
 /* ---- small device utilities used by the Python mirror of crc.py / ldpc_check ---------------- */
