@@ -383,6 +383,13 @@ __global__ __launch_bounds__(k38Threads) void k_stft3840(StftArgs a) {
   const cplx<float>* tw = reinterpret_cast<const cplx<float>*>(a.tw);            // W_1920^m
   const cplx<float>* post = reinterpret_cast<const cplx<float>*>(a.post);  // W_3840^k
   const float* win = reinterpret_cast<const float*>(a.window);
+  // twiddle seeds (registers): stage 2 W_128^k (k = t % 16), stage 3 W_1920^t, epilogue
+  // W_3840^(f_lo + t) and its 128-bin step; the powers are formed by complex recurrence each frame
+  // (relative error ~15 ulp, far inside the dB tolerance)
+  cplx<float> s2 = tw[15 * (t & 15)], s3 = tw[t];
+  const bool rec_post = a.f_lo + a.nf_out <= k38P;
+  cplx<float> p0 = post[min(a.f_lo + t, k38P)];
+  const cplx<float> pstep = post[k38Threads];
 
   // per-thread constants: the window of its 8 stage-1 pairs (twiddles come from the L1-resident table)
   const bool s1 = t < 120;
@@ -405,8 +412,8 @@ __global__ __launch_bounds__(k38Threads) void k_stft3840(StftArgs a) {
   const float scale = (float)a.scale;
   float* outb = reinterpret_cast<float*>(a.out);
   for (int f = f_begin; f < f_end; ++f) {
-    // the twiddle loads stay inside the loop (L1 hits) instead of pinning 42 registers
-    asm volatile("" : "+s"(tw));
+    // re-opaque the seeds so the per-frame twiddle powers are not hoisted into ~50 live registers
+    asm volatile("" : "+v"(s2.x), "+v"(s2.y), "+v"(s3.x), "+v"(s3.y), "+v"(p0.x), "+v"(p0.y));
     // prefetch the next frame's 4 new pairs (n + 480 = t + 120 (r + 4))
     float na[4], nb[4];
     const bool more = f + 1 < f_end;
@@ -435,8 +442,12 @@ __global__ __launch_bounds__(k38Threads) void k_stft3840(StftArgs a) {
 #pragma unroll
         for (int r = 0; r < 8; ++r) v[r] = bufA[j + 240 * r];
         if ((j & 15) != 0) {
+          cplx<float> w = s2;  // W_128^(r k)
 #pragma unroll
-          for (int r = 1; r < 8; ++r) v[r] = cmul(v[r], tw[(r * (j & 15) * 15) % k38P]);  // W_128^(r k)
+          for (int r = 1; r < 8; ++r) {
+            v[r] = cmul(v[r], w);
+            if (r < 7) w = cmul(w, s2);
+          }
         }
         Dft<8, float>::run(v);
         const int d0 = (j >> 4) * 128 + (j & 15);
@@ -451,8 +462,12 @@ __global__ __launch_bounds__(k38Threads) void k_stft3840(StftArgs a) {
 #pragma unroll
       for (int r = 0; r < 15; ++r) v[r] = bufB[t + 128 * r];
       if (t != 0) {
+        cplx<float> w = s3;  // W_1920^(r t)
 #pragma unroll
-        for (int r = 1; r < 15; ++r) v[r] = cmul(v[r], tw[(r * t) % k38P]);  // W_1920^(r t)
+        for (int r = 1; r < 15; ++r) {
+          v[r] = cmul(v[r], w);
+          if (r < 14) w = cmul(w, s3);
+        }
       }
       dft15(v, y);
 #pragma unroll
@@ -461,6 +476,7 @@ __global__ __launch_bounds__(k38Threads) void k_stft3840(StftArgs a) {
     __syncthreads();
     // epilogue: real-signal spectrum, power, dB, kept bins
     float* out = outb + ((int64_t)slot * a.nt_out + f) * a.nf_out;
+    cplx<float> pw_k = p0;  // W_3840^k for k = f_lo + i (recurrence over i += 128)
     for (int i = t; i < a.nf_out; i += k38Threads) {
       const int k = a.f_lo + i;
       const int kk = (k <= k38P) ? k : 2 * k38P - k;
@@ -468,7 +484,8 @@ __global__ __launch_bounds__(k38Threads) void k_stft3840(StftArgs a) {
       const cplx<float> Bc = bufA[kk == 0 ? 0 : k38P - kk];
       const cplx<float> B = {Bc.x, -Bc.y};
       const cplx<float> sm = cadd(A, B), df = csub(A, B);
-      const cplx<float> wd = cmul(post[kk], df);
+      const cplx<float> wd = cmul(rec_post ? pw_k : post[kk], df);
+      pw_k = cmul(pw_k, pstep);
       const cplx<float> X = {0.5f * (sm.x + wd.y), 0.5f * (sm.y - wd.x)};
       const float pw = (X.x * X.x + X.y * X.y) * scale;
       out[i] = 10.0f * log10f(1e-12f + pw);

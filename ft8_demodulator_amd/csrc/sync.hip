@@ -133,7 +133,7 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 template <int BPT, int SPS>
 struct S2Geom {
-  static constexpr int P = kS2TW + 7 * BPT + (BPT & 1);  // staged columns (even: 8-byte rows)
+  static constexpr int P = (kS2TW + 7 * BPT + 3) & ~3;   // staged columns (multiple of 4: float4 rows)
   static constexpr int H = kS2R + 8 * SPS;               // staged rows per Costas band
   static constexpr int kFloats = 3 * H * P;
 };
@@ -162,14 +162,39 @@ __global__ __launch_bounds__(kS2Threads) void k_score2(ScoreArgs a) {
   const int c0 = ct * kS2TW;
   const float* wf = reinterpret_cast<const float*>(a.wf) + (int64_t)slot * a.T * a.F;
 
-  // stage band m: waterfall rows [a0 + 36 m SPS - SPS, + H), columns [c0, c0 + P)
-  for (int i = threadIdx.x; i < G::kFloats; i += kS2Threads) {
-    const int m = i / (H * P), rem = i - m * (H * P);
-    const int rr = rem / P, cc = rem - rr * P;
-    const int row = a0 + 36 * m * SPS - SPS + rr, col = c0 + cc;
-    float v = 0.0f;
-    if (row >= 0 && row < a.T && col < a.F) v = wf[(int64_t)row * a.F + col];
-    tile[i] = v;
+  // stage band m: waterfall rows [a0 + 36 m SPS - SPS, + H), columns [c0, c0 + P).  Rows are
+  // P / 4 float4s; every thread issues all its loads before its first LDS store, so the staging
+  // costs one memory round trip (rows outside the waterfall / columns past F are zero and never
+  // read by a valid candidate)
+  if ((a.F & 3) == 0) {
+    constexpr int kVec = 3 * H * (P / 4);
+    constexpr int kIter = (kVec + kS2Threads - 1) / kS2Threads;
+    float4 v[kIter];
+#pragma unroll
+    for (int it = 0; it < kIter; ++it) {
+      const int i = threadIdx.x + it * kS2Threads;
+      v[it] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (i < kVec) {
+        const int rw = i / (P / 4), q4 = i - rw * (P / 4);
+        const int m = rw / H, rr = rw - m * H;
+        const int row = a0 + 36 * m * SPS - SPS + rr, col = c0 + 4 * q4;
+        if (row >= 0 && row < a.T && col < a.F) v[it] = *reinterpret_cast<const float4*>(wf + (int64_t)row * a.F + col);
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < kIter; ++it) {
+      const int i = threadIdx.x + it * kS2Threads;
+      if (i < kVec) reinterpret_cast<float4*>(tile)[i] = v[it];
+    }
+  } else {
+    for (int i = threadIdx.x; i < G::kFloats; i += kS2Threads) {
+      const int m = i / (H * P), rem = i - m * (H * P);
+      const int rr = rem / P, cc = rem - rr * P;
+      const int row = a0 + 36 * m * SPS - SPS + rr, col = c0 + cc;
+      float v = 0.0f;
+      if (row >= 0 && row < a.T && col < a.F) v = wf[(int64_t)row * a.F + col];
+      tile[i] = v;
+    }
   }
   __syncthreads();
 
