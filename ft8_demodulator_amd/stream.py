@@ -1,0 +1,148 @@
+"""Streaming decode of slots that arrive in host memory ("WAV ingestion + H2D
+pipelining").
+
+Batches of 15-s slots -- typically 16-bit PCM straight from WAV files -- are staged in pinned host
+memory and uploaded on a dedicated copy stream into one of two device buffers, while the previous
+batch is decoded on the compute stream; results come back through pinned host buffers.  int16 PCM
+is uploaded as-is (half the PCIe bytes of float32) and scaled by the STFT kernel exactly as
+read_wave_file does (from_wave.py:59-67).
+
+    sd = StreamDecoder(n_samples=180000, max_candidates=300, min_score=2)
+    for per_slot in sd.decode_batches(batches):      # each batch: np.int16 [B, n_samples], or a
+        ...                                          # pinned torch int16 tensor (no staging copy)
+
+decode_wave_files() is the one-call form for a list of WAV files of equal length and rate.
+"""
+from __future__ import annotations
+
+from typing import Iterable, Iterator, List
+
+import numpy as np
+
+from . import _lib
+from ._pipeline import SlotDecoder, records_to_results
+
+
+class StreamDecoder:
+    """Double-buffered host -> device upload overlapped with ft8_decode_batch."""
+
+    def __init__(self, n_samples: int, sample_rate: int = 12000, max_batch: int = 256, pcm16: bool = True,
+                 device=None, **decoder_kw):
+        torch = _lib.require_gpu()
+        self.torch = torch
+        self.dev = torch.device("cuda", _lib.device_index(device))
+        self.n = int(n_samples)
+        self.fs = int(sample_rate)
+        self.max_batch = int(max_batch)
+        self.pcm16 = bool(pcm16)
+        self.dtype = torch.int16 if pcm16 else torch.float32
+        self.dec = SlotDecoder(sample_rate=sample_rate, device=self.dev, **decoder_kw)
+        self.bpt = self.dec.kw["bins_per_tone"]
+        self.code = _lib.FT8_I16 if pcm16 else _lib.FT8_F32
+        self.copy_stream = torch.cuda.Stream(self.dev)
+        self.compute = torch.cuda.current_stream(self.dev)
+        self.dbuf = [torch.empty((self.max_batch, self.n), dtype=self.dtype, device=self.dev) for _ in range(2)]
+        self.hbuf = [torch.empty((self.max_batch, self.n), dtype=self.dtype, pin_memory=True) for _ in range(2)]
+        self.freed = [None, None]   # compute-stream event: decode done with dbuf[i]
+        cap = self.dec.cap * _lib.RESULT_DTYPE.itemsize
+        self.hout = [torch.empty(self.max_batch * cap, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
+        self.hcnt = [torch.empty(self.max_batch, dtype=torch.int32, pin_memory=True) for _ in range(2)]
+        self.ready = [None, None]   # compute-stream event: results copied to hout/hcnt[i]
+
+    def _stage(self, i: int, batch) -> int:
+        """Start the upload of a host batch into device buffer i.  A pinned torch tensor is uploaded
+        in place; anything else is first copied into pinned buffer i."""
+        torch = self.torch
+        if isinstance(batch, torch.Tensor) and batch.device.type == "cpu" and batch.is_pinned():
+            src = batch if batch.dim() == 2 else batch.unsqueeze(0)
+            if src.dtype != self.dtype or src.shape[1] != self.n or src.shape[0] > self.max_batch:
+                raise ValueError(f"pinned batch must be {self.dtype} [<= {self.max_batch}, {self.n}]")
+            nb = src.shape[0]
+            if self.freed[i] is not None:
+                self.freed[i].synchronize()
+            with torch.cuda.stream(self.copy_stream):
+                self.dbuf[i][:nb].copy_(src, non_blocking=True)
+                up = torch.cuda.Event()
+                up.record(self.copy_stream)
+            self.compute.wait_event(up)
+            return nb
+        b = np.asarray(batch)
+        if b.ndim == 1:
+            b = b[None, :]
+        if b.shape[1] != self.n or b.shape[0] > self.max_batch:
+            raise ValueError(f"batch must be [<= {self.max_batch}, {self.n}]")
+        want = np.int16 if self.pcm16 else np.float32
+        if b.dtype != want:
+            raise TypeError(f"batch dtype must be {np.dtype(want).name}")
+        nb = b.shape[0]
+        if self.freed[i] is not None:
+            self.freed[i].synchronize()          # the decode that last read dbuf[i] is done
+        self.hbuf[i][:nb].numpy()[...] = b
+        with torch.cuda.stream(self.copy_stream):
+            self.dbuf[i][:nb].copy_(self.hbuf[i][:nb], non_blocking=True)
+            up = torch.cuda.Event()
+            up.record(self.copy_stream)
+        self.compute.wait_event(up)
+        return nb
+
+    def _launch(self, i: int, nb: int):
+        torch = self.torch
+        with torch.cuda.stream(self.compute):
+            out, cnt = self.dec.run(self.dbuf[i][:nb], code=self.code)
+            ev = torch.cuda.Event()
+            ev.record(self.compute)
+            self.freed[i] = ev
+            cap = self.dec.cap * _lib.RESULT_DTYPE.itemsize
+            self.hout[i][: nb * cap].copy_(out[: nb * cap], non_blocking=True)
+            self.hcnt[i][:nb].copy_(cnt[:nb], non_blocking=True)
+            r = torch.cuda.Event()
+            r.record(self.compute)
+            self.ready[i] = r
+
+    def _collect(self, i: int, nb: int) -> List[list]:
+        self.ready[i].synchronize()
+        cap = self.dec.cap
+        recs = self.hout[i][: nb * cap * _lib.RESULT_DTYPE.itemsize].numpy().view(_lib.RESULT_DTYPE).reshape(nb, cap)
+        cnt = self.hcnt[i][:nb].numpy()
+        return [records_to_results(recs[s, : min(int(cnt[s]), cap)].copy(), self.fs, self.bpt, False)
+                for s in range(nb)]
+
+    def decode_batches(self, batches: Iterable) -> Iterator[List[list]]:
+        """Yield per-slot results of each batch, in order; batch k+1 uploads while batch k decodes."""
+        pending = None
+        for k, batch in enumerate(batches):
+            i = k % 2
+            nb = self._stage(i, batch)
+            self._launch(i, nb)
+            if pending is not None:
+                yield self._collect(*pending)
+            pending = (i, nb)
+        if pending is not None:
+            yield self._collect(*pending)
+
+
+def decode_wave_files(paths: List[str], batch: int = 256, device=None, **decoder_kw) -> List[list]:
+    """Decode many 16-bit PCM WAV files of one sample rate and length -> results per file."""
+    from .from_wave import _read_raw
+    if not paths:
+        return []
+    first, dt, fs = _read_raw(paths[0])
+    if dt != np.int16:
+        raise TypeError("decode_wave_files expects 16-bit PCM")
+    n = first.shape[0]
+
+    def batches():
+        for b0 in range(0, len(paths), batch):
+            arr = np.empty((min(batch, len(paths) - b0), n), dtype=np.int16)
+            for j, p in enumerate(paths[b0:b0 + arr.shape[0]]):
+                d, dt2, fs2 = _read_raw(p)
+                if dt2 != np.int16 or fs2 != fs or d.shape[0] != n:
+                    raise ValueError(f"{p}: every file must be 16-bit PCM at {fs} Hz with {n} samples")
+                arr[j] = d
+            yield arr
+
+    sd = StreamDecoder(n, sample_rate=fs, max_batch=min(batch, len(paths)), pcm16=True, device=device, **decoder_kw)
+    out: List[list] = []
+    for res in sd.decode_batches(batches()):
+        out.extend(res)
+    return out

@@ -125,3 +125,27 @@ def test_pipeline_settings_do_not_change_results(gpu):
     assert sum(np.frombuffer(base[1], np.int32)) > 0
     for cfg, v in got.items():
         assert v == base, cfg
+
+
+def test_stream_decoder_matches_resident_decode(gpu):
+    """Host PCM batches through the double-buffered upload path == decoding the same int16 slots
+    already resident on the GPU (and the per-file WAV helper == decode_ft8_from_wave)."""
+    import torch
+    from ft8_demodulator_amd import SlotDecoder, synth
+    from ft8_demodulator_amd.stream import StreamDecoder, decode_wave_files
+    x, _ = synth.make_slots(24, 20, seed=99, device="cuda")
+    pcm = torch.clamp(torch.round(x / x.abs().amax() * 30000.0), -32767, 32767).to(torch.int16).cpu().numpy()
+    kw = dict(max_candidates=100, min_score=3, max_iterations=20)
+    ref = SlotDecoder(12000, **kw).decode(torch.from_numpy(pcm).cuda())
+    sd = StreamDecoder(pcm.shape[1], max_batch=8, **kw)
+    got = []
+    for res in sd.decode_batches([pcm[0:8], pcm[8:16], pcm[16:24]]):
+        got.extend(res)
+    key = lambda rs: [[(m.payload.hex(), s.crc_calculated, t, f, float(sc)) for (m, s, t, f, sc) in r] for r in rs]
+    assert key(got) == key(ref)
+    assert sum(len(r) for r in got) > 0
+    from ft8_demodulator_amd import decode_ft8_from_wave
+    wavs = [os.path.join(DATA, n) for n in ("synth_cfg1.wav", "synth_cfg2.wav")]
+    files = decode_wave_files(wavs, batch=2)
+    for w, r in zip(wavs, files):
+        assert key([r]) == key([decode_ft8_from_wave(w)])
