@@ -149,25 +149,27 @@ __device__ __forceinline__ void div_rn(double* q, const double* x, const double*
 // (the workgroup is one lockstep wave), so toc can overwrite tov in place and vice versa.  Edge
 // position e lives at msg[2e]; msg[2e + 1] is a constant 1.0, which stands in for the missing sixth
 // product factor of a degree-6 check (the companion of its position 5).
+constexpr int kZeroBit = 255;  // bits[255] is never written: the padding checks' variable
 struct WaveLds {
-  double c[kVarPad];
-  double msg[2 * (kEdgePad + 8)];  // tov between sweeps / toc between the two phases of a sweep
+  double msg[2 * (kEdgePad + 8)];  // tov between sweeps; V->C arguments, then toc, within a sweep
   uint64_t poff[16];               // [k + 7 * (degree == 6)]: byte offsets of the 6 product factors
-  uint64_t ebits[kEdgeSlots + 1];  // hard decision of every edge's variable, one bit per edge
-  uint8_t bits[256];
+  uint8_t bits[256];               // hard decision of every variable (last evaluated sweep)
   uint8_t a91[16];
 };
 
-// Per-lane edge tables (registers, loaded once per wave).
-//   vc: variable n | first other edge << 8 | second other edge << 18 | pos2 << 28 | first << 29
-//       (others in the variable's check order; pos2: this edge is the variable's third edge;
-//        first: this edge is the variable's first edge -- it reports the hard decision)
-//   cv: LDS byte address of the check's row (&msg[2 * start]) | LDS address of its poff entry << 16
-//   ck: check start | degree << 10 for the lane's two check slots (degree 0: padding)
+// Per-lane tables (registers, loaded once per wave).  A sweep runs in two layouts:
+//   variable-major (3 slots, variable n = lane + 64 j): hard decision and variable->check sums
+//     va: LDS byte address of the variable's 1st edge message | 2nd edge << 16 (check order)
+//     vb: LDS byte address of its 3rd edge message
+//   edge-major (9 slots, edge e = lane + 64 i): fast_tanh, check products, fast_atanh
+//     cv: LDS byte address of the check's row (&msg[2 * start]) | LDS address of its poff entry << 16
+//   check-major (2 slots, check m = lane + 64 k): parity
+//     pk: the check's variables, one byte each (7; a degree-6 check's 7th is kZeroBit)
 struct WaveTables {
-  uint32_t vc[kEdgeSlots];
+  uint32_t va[kVarSlots];
+  uint32_t vb[kVarSlots];
   uint32_t cv[kEdgeSlots];
-  uint32_t ck[kChkSlots];
+  uint32_t pk[kChkSlots][2];
 };
 
 __device__ __forceinline__ uint32_t lds_addr(const void* p) {
@@ -191,43 +193,53 @@ __device__ void init_poff(WaveLds& L, int lane) {
 
 __device__ void load_tables(WaveTables& t, const WaveLds& L, int lane) {
   const uint32_t msg0 = lds_addr(&L.msg[0]), poff0 = lds_addr(&L.poff[0]);
+  const uint32_t dummy = msg0 + 16u * (kEdgePad - 1);  // padding variables use a padding edge
+#pragma unroll
+  for (int j = 0; j < kVarSlots; ++j) {
+    const int n = lane + kWave * j;
+    if (n < FT8_LDPC_N) {
+      t.va[j] = (msg0 + 16u * kVarEdgeD[3 * n]) | ((msg0 + 16u * kVarEdgeD[3 * n + 1]) << 16);
+      t.vb[j] = msg0 + 16u * kVarEdgeD[3 * n + 2];
+    } else {
+      t.va[j] = dummy | (dummy << 16);
+      t.vb[j] = dummy;
+    }
+  }
 #pragma unroll
   for (int i = 0; i < kEdgeSlots; ++i) {
     const int e = lane + kWave * i;
     if (e < FT8_LDPC_E) {
-      const int n = kEdgeVarD[e];
-      int o[2], k = 0, pos = 0;
-      for (int j = 0; j < 3; ++j) {
-        const int ej = kVarEdgeD[3 * n + j];
-        if (ej != e) o[k++] = ej;
-        else pos = j;
-      }
-      t.vc[i] = (uint32_t)n | ((uint32_t)o[0] << 8) | ((uint32_t)o[1] << 18) | ((uint32_t)(pos == 2) << 28) |
-                ((uint32_t)(pos == 0) << 29);
       const int m = kEdgeChkD[e];
       const int s = kChkStartD[m], d = kChkStartD[m + 1] - s;
       const uint32_t entry = (uint32_t)(e - s) + (d == 6 ? 7u : 0u);
       t.cv[i] = (msg0 + 16u * (uint32_t)s) | ((poff0 + 8u * entry) << 16);
-    } else {  // padding edge: reads c[174] and msg[522], its check is the padding block at 522
-      t.vc[i] = (uint32_t)FT8_LDPC_N | ((uint32_t)FT8_LDPC_E << 8) | ((uint32_t)FT8_LDPC_E << 18);
+    } else {  // padding edge: its check is the padding block at 522
       const uint32_t k = (uint32_t)(e - FT8_LDPC_E) % 7u;
       t.cv[i] = (msg0 + 16u * (uint32_t)FT8_LDPC_E) | ((poff0 + 8u * k) << 16);
     }
   }
 #pragma unroll
-  for (int i = 0; i < kChkSlots; ++i) {
-    const int m = lane + kWave * i;
-    t.ck[i] = 0;
-    if (m < FT8_LDPC_M) {
-      const int s = kChkStartD[m], d = kChkStartD[m + 1] - s;
-      t.ck[i] = (uint32_t)s | ((uint32_t)d << 10);
+  for (int k = 0; k < kChkSlots; ++k) {
+    const int m = lane + kWave * k;
+    uint32_t w[2] = {0, 0};
+    for (int q = 0; q < 7; ++q) {
+      uint32_t v = kZeroBit;
+      if (m < FT8_LDPC_M) {
+        const int s = kChkStartD[m], d = kChkStartD[m + 1] - s;
+        if (q < d) v = kEdgeVarD[s + q];
+      }
+      w[q >> 2] |= v << (8 * (q & 3));
     }
+    t.pk[k][0] = w[0];
+    t.pk[k][1] = w[1];
   }
   // keep the tables in registers: opaque values cannot be rematerialised from memory in the loop
 #pragma unroll
-  for (int i = 0; i < kEdgeSlots; ++i) asm volatile("" : "+v"(t.vc[i]), "+v"(t.cv[i]));
+  for (int j = 0; j < kVarSlots; ++j) asm volatile("" : "+v"(t.va[j]), "+v"(t.vb[j]));
 #pragma unroll
-  for (int i = 0; i < kChkSlots; ++i) asm volatile("" : "+v"(t.ck[i]));
+  for (int i = 0; i < kEdgeSlots; ++i) asm volatile("" : "+v"(t.cv[i]));
+#pragma unroll
+  for (int k = 0; k < kChkSlots; ++k) asm volatile("" : "+v"(t.pk[k][0]), "+v"(t.pk[k][1]));
 }
 
 struct BpArgs {
@@ -348,11 +360,12 @@ __global__ __launch_bounds__(kWave, BP_WAVES_PER_EU) void k_bp(BpArgs a) {
   WaveTables tb;
   load_tables(tb, L, lane);
   init_poff(L, lane);
-  for (int n = lane; n < kVarPad; n += kWave) L.c[n] = 0.0;
   for (int n = lane; n < 256; n += kWave) L.bits[n] = 0;
   for (int e = lane; e < kEdgePad + 8; e += kWave) L.msg[2 * e + 1] = 1.0;
-  if (lane == 0) L.ebits[kEdgeSlots] = 0;
   __syncthreads();
+  // edge slot 8 holds edges 512..575: lanes >= 10 are padding; their V->C argument is pinned to
+  // 1.0 so the padding keeps every numerator of the division fast path non-zero
+  const bool pad8 = lane + kWave * (kEdgeSlots - 1) >= FT8_LDPC_E;
 
   // work counters, per wave; flushed once when the wave retires (same-address atomics per
   // candidate would serialise in L2)
@@ -373,83 +386,75 @@ __global__ __launch_bounds__(kWave, BP_WAVES_PER_EU) void k_bp(BpArgs a) {
       af = a.cand[((int64_t)slot * a.N + cidx) * 2 + 1];
       score = a.cand_score[(int64_t)slot * a.N + cidx];
     }
-    for (int n = lane; n < FT8_LDPC_N; n += kWave) L.c[n] = a.llr_in[(int64_t)item * FT8_LDPC_N + n];
+    double cv_[kVarSlots];  // codeword[n] (the LLR) of the lane's variables
+#pragma unroll
+    for (int j = 0; j < kVarSlots; ++j) {
+      const int n = lane + kWave * j;
+      cv_[j] = n < FT8_LDPC_N ? a.llr_in[(int64_t)item * FT8_LDPC_N + n] : 0.0;
+    }
 
     // ---- belief propagation (ldpc_decoder.py:54-113) ----------------------------------------
-    // One sweep = the reference iteration: hard decision + checks on the current tov, then
-    // variable->check and check->variable messages.  Fused per edge lane: the gather that feeds
-    // the variable->check sum also yields the variable's hard decision (the lane keeps its own
-    // tov in a register), so the decision costs no extra LDS traffic.
+    // One sweep = the reference iteration.  (A) variable-major: each lane reads its variables'
+    // three tov, forms the hard decision c + ((t0 + t1) + t2) and the three variable->check sums
+    // (c + t_a) + t_b, and writes the clipped -T/2 into each edge's slot; (B) parity per check from
+    // the decision bytes; (C) edge-major: fast_tanh -> toc; (D) check products -> fast_atanh -> tov.
     for (int e = lane; e < kEdgePad + 8; e += kWave) L.msg[2 * e] = 0.0;
-    if (lane <= kEdgeSlots) L.ebits[lane] = 0;  // the hard decision if no sweep runs
+    for (int n = lane; n < kVarPad; n += kWave) L.bits[n] = 0;  // the hard decision if no sweep runs
     __syncthreads();
-    double tv[kEdgeSlots];
-#pragma unroll
-    for (int i = 0; i < kEdgeSlots; ++i) tv[i] = 0.0;
     int min_errors = FT8_LDPC_M;
     int entered = 0, passes = 0;
     for (int iter = 0; iter < a.max_iterations; ++iter) {
       entered++;
-      // re-opaque the tables every sweep: otherwise the compiler hoists all 90 derived LDS
-      // addresses out of the loop (spilling); recomputing them is a few integer ops
+      // re-opaque the tables every sweep: otherwise the compiler hoists the derived LDS addresses
+      // out of the loop (spilling); recomputing them is one integer op each
 #pragma unroll
-      for (int i = 0; i < kEdgeSlots; ++i) asm volatile("" : "+v"(tb.vc[i]), "+v"(tb.cv[i]));
+      for (int j = 0; j < kVarSlots; ++j) asm volatile("" : "+v"(tb.va[j]), "+v"(tb.vb[j]));
 #pragma unroll
-      for (int i = 0; i < kChkSlots; ++i) asm volatile("" : "+v"(tb.ck[i]));
-      double x[kEdgeSlots];
-      uint64_t hd[kEdgeSlots];  // wave ballots: hard decision of every edge's variable
-      {
-        double tc[kEdgeSlots], ta[kEdgeSlots], tb2[kEdgeSlots];
+      for (int i = 0; i < kEdgeSlots; ++i) asm volatile("" : "+v"(tb.cv[i]));
 #pragma unroll
-        for (int i = 0; i < kEdgeSlots; ++i) {
-          const uint32_t v = tb.vc[i];
-          tc[i] = L.c[v & 255];
-          ta[i] = L.msg[2 * ((v >> 8) & 1023)];
-          tb2[i] = L.msg[2 * ((v >> 18) & 1023)];
-        }
+      for (int k = 0; k < kChkSlots; ++k) asm volatile("" : "+v"(tb.pk[k][0]), "+v"(tb.pk[k][1]));
+      // (A) hard decision + variable -> check arguments
+      uint64_t any = 0;
 #pragma unroll
-        for (int i = 0; i < kEdgeSlots; ++i) {
-          const bool p2 = (tb.vc[i] >> 28) & 1u;
-          // messages = codeword + sum(tov, axis=1): c + ((t0 + t1) + t2) in the variable's order:
-          // own edge first or second -> (own + oa) + ob; own edge third -> (oa + ob) + own
-          const double u = p2 ? tb2[i] : tv[i];
-          const double hs = (ta[i] + u) + (p2 ? tv[i] : tb2[i]);
-          hd[i] = __ballot((tc[i] + hs) > 0.0);
-          // variable -> check input: Tnm = c[n] + other1 + other2 (ldpc_decoder.py:93-96)
-          double t = tc[i];
-          t += ta[i];
-          t += tb2[i];
-          x[i] = __builtin_fmin(__builtin_fmax(-t / 2, -4.97), 4.97);  // np.clip (no NaN reaches here)
-        }
+      for (int j = 0; j < kVarSlots; ++j) {
+        const uint32_t a0 = tb.va[j] & 0xFFFFu, a1 = tb.va[j] >> 16, a2 = tb.vb[j];
+        const double t0 = *(lds_f64*)(uintptr_t)a0;
+        const double t1 = *(lds_f64*)(uintptr_t)a1;
+        const double t2 = *(lds_f64*)(uintptr_t)a2;
+        const double c = cv_[j];
+        // messages = codeword + sum(tov, axis=1) (ldpc_decoder.py:72-73)
+        const bool bit = (c + ((t0 + t1) + t2)) > 0.0;
+        const uint64_t bal = __ballot(bit);
+        any |= j == kVarSlots - 1 ? bal & ((1ull << (FT8_LDPC_N - kWave * (kVarSlots - 1))) - 1ull) : bal;
+        L.bits[lane + kWave * j] = (uint8_t)bit;
+        // Tnm = codeword[n] + the other two tov in check order (ldpc_decoder.py:90-96)
+        const double c0 = c + t0;
+        const double T0 = (c + t1) + t2, T1 = c0 + t2, T2 = c0 + t1;
+        // fast_tanh's np.clip (no NaN reaches here)
+        *(__attribute__((address_space(3))) double*)(uintptr_t)a0 = __builtin_fmin(__builtin_fmax(-T0 / 2, -4.97), 4.97);
+        *(__attribute__((address_space(3))) double*)(uintptr_t)a1 = __builtin_fmin(__builtin_fmax(-T1 / 2, -4.97), 4.97);
+        *(__attribute__((address_space(3))) double*)(uintptr_t)a2 = __builtin_fmin(__builtin_fmax(-T2 / 2, -4.97), 4.97);
       }
-      // publish the edge bits for the parity check and the final hard decision
-      if (lane == 0) {
-#pragma unroll
-        for (int i = 0; i < kEdgeSlots; ++i) L.ebits[i] = hd[i];
-      }
-      // all-zero hard decision -> stop (ldpc_decoder.py:76-78); padding edges (slot 8, lanes >= 10)
-      // never count
-      uint64_t any = hd[kEdgeSlots - 1] & ((1ull << (FT8_LDPC_E - kWave * (kEdgeSlots - 1))) - 1ull);
-#pragma unroll
-      for (int i = 0; i < kEdgeSlots - 1; ++i) any |= hd[i];
       __syncthreads();
+      // all-zero hard decision -> stop (ldpc_decoder.py:76-78)
       if (any == 0) break;
-      // parity check (ldpc_check, ldpc_decoder.py:33-52): a check's edges are contiguous
+      // (B) parity check (ldpc_check, ldpc_decoder.py:33-52)
       int errs = 0;
 #pragma unroll
-      for (int i = 0; i < kChkSlots; ++i) {
-        const uint32_t ck = tb.ck[i];
-        const int s0 = ck & 1023, d = ck >> 10;
-        const uint64_t lo = L.ebits[s0 >> 6], hi = L.ebits[(s0 >> 6) + 1];
-        const int sh = s0 & 63;
-        const uint64_t w = sh ? ((lo >> sh) | (hi << (64 - sh))) : lo;
-        const uint64_t bitsd = w & ((1ull << d) - 1ull);
-        errs += __popcll(__ballot(__popcll(bitsd) & 1));
+      for (int k = 0; k < kChkSlots; ++k) {
+        unsigned par = 0;
+#pragma unroll
+        for (int q = 0; q < 7; ++q) par ^= L.bits[(tb.pk[k][q >> 2] >> (8 * (q & 3))) & 0xFFu];
+        errs += __popcll(__ballot(par & 1u));
       }
       if (errs < min_errors) {
         min_errors = errs;
         if (errs == 0) break;
       }
+      double x[kEdgeSlots];
+#pragma unroll
+      for (int i = 0; i < kEdgeSlots; ++i) x[i] = L.msg[2 * (lane + kWave * i)];
+      x[kEdgeSlots - 1] = pad8 ? 1.0 : x[kEdgeSlots - 1];
       // variable -> check messages: toc = fast_tanh(-Tnm / 2), three interleaved divisions at a time
 #pragma unroll
       for (int g = 0; g < kEdgeSlots; g += kDivGroup) {
@@ -496,19 +501,11 @@ __global__ __launch_bounds__(kWave, BP_WAVES_PER_EU) void k_bp(BpArgs a) {
         div_rn<kDivGroup>(&x[g], na, nb);
       }
 #pragma unroll
-      for (int i = 0; i < kEdgeSlots; ++i) {
-        tv[i] = -2 * x[i];
-        L.msg[2 * (lane + kWave * i)] = tv[i];
-      }
+      for (int i = 0; i < kEdgeSlots; ++i) L.msg[2 * (lane + kWave * i)] = -2 * x[i];
       passes++;
       __syncthreads();
     }
-    // hard decision of the last evaluated sweep -> bits[n], reported by each variable's first edge
-#pragma unroll
-    for (int i = 0; i < kEdgeSlots; ++i) {
-      const uint32_t v = tb.vc[i];
-      if ((v >> 29) & 1u) L.bits[v & 255] = (uint8_t)((L.ebits[i] >> lane) & 1u);
-    }
+    // bits[] holds the hard decision of the last evaluated sweep
     __syncthreads();
     st_cand++;
     st_iter += entered;
