@@ -91,35 +91,43 @@ __device__ __forceinline__ double pymax4(double a, double b, double c, double d)
 // quotient unchanged for finite normal operands and quotient.  Every denominator here lies in
 // [67, 2.1e4] (fast_tanh: 945 + x^2 (420 + 15 x^2) with |x| <= 4.97; fast_atanh: 945 + x^2 (-1050 +
 // 225 x^2) with |x| <= 1.0072^6) and every numerator below 2.1e4, so when every numerator of the
-// wave satisfies |x| >= 2^-960 the scale/fmas/fixup steps are identities and the short sequence below produces the same
-// bits (measured: ~59 vs ~78 SIMD-cycles per wave division).  Otherwise the full sequence runs.
-template <int N>
-__device__ __forceinline__ void div_rn(double* q, const double* x, const double* y) {
+// wave satisfies |x| >= 2^-960 the scale/fmas/fixup steps are identities and the short sequence
+// below produces the same bits (measured: ~59 vs ~78 SIMD-cycles per wave division).  Otherwise
+// the full sequence runs.
+//
+// NEG2: y holds -b/2 for the reference's denominator b and the result is -2 RN(x/b) (fast_atanh's
+// caller scales by -2, ldpc_decoder.py:108).  On the fast path every quotient is normal, so
+// RN(x / (-b/2)) == -2 RN(x/b) exactly and the scaling costs nothing; the full path divides by
+// b = -2 y (exact) and scales the quotient.
+template <int N, bool NEG2 = false>
+__device__ __forceinline__ void div_rn(double* q, const double* x, const double* y_in) {
   bool safe = true;  // |x| < 2^900 always holds here (clamped / bounded inputs); NaN fails the test
 #pragma unroll
   for (int i = 0; i < N; ++i) safe = safe && (__builtin_fabs(x[i]) >= 0x1p-960);
   double r[N], e[N], m[N];
   if (__all(safe)) {
 #pragma unroll
-    for (int i = 0; i < N; ++i) r[i] = __builtin_amdgcn_rcp(y[i]);
+    for (int i = 0; i < N; ++i) r[i] = __builtin_amdgcn_rcp(y_in[i]);
 #pragma unroll
-    for (int i = 0; i < N; ++i) e[i] = __builtin_fma(-y[i], r[i], 1.0);
+    for (int i = 0; i < N; ++i) e[i] = __builtin_fma(-y_in[i], r[i], 1.0);
 #pragma unroll
     for (int i = 0; i < N; ++i) r[i] = __builtin_fma(r[i], e[i], r[i]);
 #pragma unroll
-    for (int i = 0; i < N; ++i) e[i] = __builtin_fma(-y[i], r[i], 1.0);
+    for (int i = 0; i < N; ++i) e[i] = __builtin_fma(-y_in[i], r[i], 1.0);
 #pragma unroll
     for (int i = 0; i < N; ++i) r[i] = __builtin_fma(r[i], e[i], r[i]);
 #pragma unroll
     for (int i = 0; i < N; ++i) m[i] = x[i] * r[i];
 #pragma unroll
-    for (int i = 0; i < N; ++i) e[i] = __builtin_fma(-y[i], m[i], x[i]);
+    for (int i = 0; i < N; ++i) e[i] = __builtin_fma(-y_in[i], m[i], x[i]);
 #pragma unroll
     for (int i = 0; i < N; ++i) q[i] = __builtin_fma(e[i], r[i], m[i]);
     return;
   }
-  double den[N], num[N];
+  double den[N], num[N], y[N];
   bool f0[N], f1[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) y[i] = NEG2 ? -2.0 * y_in[i] : y_in[i];
 #pragma unroll
   for (int i = 0; i < N; ++i) den[i] = __builtin_amdgcn_div_scale(x[i], y[i], false, &f0[i]);
 #pragma unroll
@@ -142,6 +150,10 @@ __device__ __forceinline__ void div_rn(double* q, const double* x, const double*
   for (int i = 0; i < N; ++i) q[i] = __builtin_amdgcn_div_fmas(e[i], r[i], m[i], f1[i]);
 #pragma unroll
   for (int i = 0; i < N; ++i) q[i] = __builtin_amdgcn_div_fixup(q[i], y[i], x[i]);
+  if constexpr (NEG2) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) q[i] = -2.0 * q[i];
+  }
   (void)f0;
 }
 
@@ -496,12 +508,14 @@ __global__ __launch_bounds__(kWave, BP_WAVES_PER_EU) void k_bp(BpArgs a) {
         for (int i = 0; i < kDivGroup; ++i) {
           const double xv = x[g + i], x2 = xv * xv;
           na[i] = xv * (945.0 + x2 * (-735.0 + x2 * 64.0));
-          nb[i] = (945.0 + x2 * (-1050.0 + x2 * 225.0));
+          // -b/2 for b = 945 + x2 (-1050 + x2 225): every step is the reference's step scaled by
+          // -1/2, exact (terms too small to scale exactly are absorbed by the constant they meet)
+          nb[i] = (-472.5 + x2 * (525.0 + x2 * -112.5));
         }
-        div_rn<kDivGroup>(&x[g], na, nb);
+        div_rn<kDivGroup, true>(&x[g], na, nb);  // tov = -2 fast_atanh(Tmn)
       }
 #pragma unroll
-      for (int i = 0; i < kEdgeSlots; ++i) L.msg[2 * (lane + kWave * i)] = -2 * x[i];
+      for (int i = 0; i < kEdgeSlots; ++i) L.msg[2 * (lane + kWave * i)] = x[i];
       passes++;
       __syncthreads();
     }
