@@ -242,6 +242,20 @@ def main():
     if world == 1 and not args.no_h2d:
         stream = h2d_stream(x, max(3, min(args.steps, 10)), kw)
 
+    # HBM bytes per launch from the committed rocprofv3 PMC summary (tools/pmc_traffic.py; FETCH_SIZE
+    # and WRITE_SIZE passes of the same 256-slot workload), or null when it is absent
+    traffic = {}
+    tpath = os.path.join(ROOT, "profiles", "r1_pmc_traffic.json")
+    if os.path.exists(tpath):
+        with open(tpath) as f:
+            traffic = json.load(f).get("kernels", {})
+
+    def hbm(kernel_prefix):
+        for k, v in traffic.items():
+            if k.startswith(kernel_prefix):
+                return v.get("hbm_bytes")
+        return None
+
     line = {
         "metric": METRIC,
         "value": value,
@@ -264,11 +278,11 @@ def main():
         "decodes_per_step": decoded / K,
         "roofline": {"kernel": "k_bp (float64 BP + CRC)", "bound": "fp64-valu",
                      "achieved": ach_tf, "peak": FP64_VECTOR_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": ach_tf / FP64_VECTOR_PEAK_TFLOPS, "traffic": None,
+                     "frac": ach_tf / FP64_VECTOR_PEAK_TFLOPS, "traffic": hbm("ft8::k_bp"),
                      "flops_per_launch": flops, "launch_ms": bp_ms,
                      "bp_passes_per_launch": cn["passes"] / K, "candidates_per_launch": cn["candidates"] / K},
         "roofline_hbm": {"kernel": "k_stft", "bound": "hbm", "achieved": stft_gbs, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": stft_gbs / HBM_PEAK_GBS, "traffic": None,
+                         "unit": "GB/s", "frac": stft_gbs / HBM_PEAK_GBS, "traffic": hbm("ft8::k_stft"),
                          "bytes_per_launch": stft_bytes, "launch_ms": stft_ms},
         "stages_ms": stage_ms,
         "bp_stress": stress,

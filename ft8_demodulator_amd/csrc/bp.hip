@@ -260,7 +260,7 @@ struct BpArgs {
   const int32_t* cand;
   const double* cand_score;
   const int32_t* cand_count;
-  int N, n_items, mode;
+  int N, n_items, mode, n_slots;
   const double* llr_in;
   int normalize, max_iterations;
   double* llr_out;
@@ -329,13 +329,17 @@ __global__ __launch_bounds__(kWave) void k_llr(BpArgs a) {
   __shared__ double sq[FT8_LDPC_N + 2];
   __shared__ double part[16];
   const int lane = threadIdx.x;
-  const int item = blockIdx.x;
-  if (item >= a.n_items) return;
+  int item = blockIdx.x;
   int slot = 0, at = 0, af = 0;
   if (a.mode == 0) {
-    slot = item / a.N;
-    const int cidx = item % a.N;
-    if (cidx >= a.cand_count[slot]) return;
+    // workgroup id -> (slot, candidate) with slot % 8 == id % 8: all candidates of a slot run on
+    // one XCD, so its waterfall rows are fetched into one L2 (round-robin ids would pull every
+    // slot into all eight)
+    const int q = blockIdx.x >> 3;
+    slot = (q / a.N) * 8 + (blockIdx.x & 7);
+    const int cidx = q % a.N;
+    if (slot >= a.n_slots || cidx >= a.cand_count[slot]) return;
+    item = slot * a.N + cidx;
     at = a.cand[((int64_t)slot * a.N + cidx) * 2];
     af = a.cand[((int64_t)slot * a.N + cidx) * 2 + 1];
   } else if (a.mode == 1) {
@@ -343,6 +347,7 @@ __global__ __launch_bounds__(kWave) void k_llr(BpArgs a) {
     at = a.cand[(int64_t)item * 3 + 1];
     af = a.cand[(int64_t)item * 3 + 2];
   }
+  else if (item >= a.n_items) return;
   if (a.mode == 2) {
     for (int n = lane; n < FT8_LDPC_N; n += kWave) c[n] = a.llr_in[(int64_t)item * FT8_LDPC_N + n];
   } else {
@@ -645,6 +650,7 @@ BpArgs make_args(const BpLaunch& L) {
   a.cand_count = L.cand_count;
   a.N = L.N;
   a.n_items = L.n_items;
+  a.n_slots = L.n_slots;
   a.mode = L.mode;
   a.llr_in = L.llr_in;
   a.normalize = L.normalize;
@@ -663,10 +669,11 @@ BpArgs make_args(const BpLaunch& L) {
 hipError_t launch_llr(const BpLaunch& L, hipStream_t s) {
   if (L.n_items <= 0) return hipSuccess;
   BpArgs a = make_args(L);
+  const int64_t grid = L.mode == 0 ? (int64_t)((L.n_slots + 7) / 8) * 8 * L.N : L.n_items;
   if (L.wf_f64)
-    hipLaunchKernelGGL(k_llr<double>, dim3(L.n_items), dim3(kWave), 0, s, a);
+    hipLaunchKernelGGL(k_llr<double>, dim3((unsigned)grid), dim3(kWave), 0, s, a);
   else
-    hipLaunchKernelGGL(k_llr<float>, dim3(L.n_items), dim3(kWave), 0, s, a);
+    hipLaunchKernelGGL(k_llr<float>, dim3((unsigned)grid), dim3(kWave), 0, s, a);
   return hipGetLastError();
 }
 
