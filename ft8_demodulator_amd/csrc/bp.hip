@@ -390,7 +390,8 @@ __global__ __launch_bounds__(kWave, BP_WAVES_PER_EU) void k_bp(BpArgs a) {
   for (;;) {
     unsigned item = 0;
     if (lane == 0) item = atomicAdd(a.work, 1u);
-    item = __shfl(item, 0);
+    // wave-uniform: candidate metadata then lives in SGPRs (scalar loads), not VGPRs
+    item = __builtin_amdgcn_readfirstlane(__shfl(item, 0));
     if ((int)item >= a.n_items) break;
 
     int slot = 0, at = 0, af = 0, cidx = 0;
@@ -536,12 +537,15 @@ __global__ __launch_bounds__(kWave, BP_WAVES_PER_EU) void k_bp(BpArgs a) {
       for (int n = lane; n < FT8_LDPC_N; n += kWave) a.plain_out[(int64_t)item * FT8_LDPC_N + n] = L.bits[n];
     if (a.res) {
       // pack 91 bits MSB first (ft8_decode.py:200-215)
-      if (lane < 12) {
+      if (lane < 12) {  // lane l packs decision bytes 8l..8l+7 (one 8-byte LDS read)
+        const uint64_t w = *reinterpret_cast<const uint64_t*>(&L.bits[8 * lane]);
+        const uint32_t lo = (uint32_t)w, hi = (uint32_t)(w >> 32);
         unsigned byte = 0;
-        for (int j = 0; j < 8; ++j) {
-          const int bi = lane * 8 + j;
-          if (bi < 91 && L.bits[bi]) byte |= 0x80u >> j;
-        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) byte |= ((lo >> (8 * j)) & 1u) << (7 - j);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) byte |= ((hi >> (8 * j)) & 1u) << (3 - j);
+        if (lane == 11) byte &= 0xE0u;  // bits 88..90 end the 91-bit message
         L.a91[lane] = (uint8_t)byte;
       }
       __syncthreads();
