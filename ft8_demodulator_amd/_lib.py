@@ -16,7 +16,6 @@ LIB_PATH = os.environ.get("FT8HIP_LIB", os.path.join(_HERE, "lib", "libft8hip.so
 
 FT8_F32, FT8_F64, FT8_C64, FT8_C128, FT8_I16 = 0, 1, 2, 3, 4
 FT8_OK, FT8_E_ARG, FT8_E_HIP, FT8_E_UNSUPPORTED, FT8_E_NOMEM, FT8_E_RANGE = 0, -1, -2, -3, -4, -5
-FT8_FLAG_TOPK = 1
 N_STAGES = 7
 STAGE_NAMES = ("stft", "score", "select", "bp", "compact", "decode_batch", "llr")
 

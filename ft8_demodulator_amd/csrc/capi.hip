@@ -361,7 +361,7 @@ int sync_select_core(ft8_ctx* c, const void* d_wf, int wf_f64, int n_slots, int 
 int do_sync_select(ft8_ctx* c, const void* d_wf, int wf_f64, int n_slots, int T, int F, const ft8_params* p,
                    int32_t* cand, double* cand_score, int32_t* cand_count, void* d_scores, hipStream_t s) {
   if (p->steps_per_symbol <= 0 || p->bins_per_tone <= 0) return fail(c, FT8_E_ARG, "bad oversampling factors");
-  if (p->flags & FT8_FLAG_TOPK) return fail(c, FT8_E_UNSUPPORTED, "FT8_FLAG_TOPK is not implemented yet");
+  if (p->flags != 0) return fail(c, FT8_E_ARG, "ft8_params.flags is reserved and must be 0");
   const int N = p->max_candidates;
   if (N > kMaxCandidates)
     return fail(c, FT8_E_RANGE, "max_candidates > " + std::to_string(kMaxCandidates) + " is not supported");
@@ -405,7 +405,6 @@ int sync_select_core(ft8_ctx* c, const void* d_wf, int wf_f64, int n_slots, int 
   L.N = N;
   L.min_score = p->min_score;
   L.min_score_f64 = p->min_score_f64;
-  L.flags = p->flags;
   L.cand = cand;
   L.cand_score = cand_score;
   L.cand_count = cand_count;
@@ -609,7 +608,7 @@ int ft8_decode_batch(ft8_ctx* c, const void* d_samples, int dtype, int64_t n_sam
   if ((rc = ensure(c, c->warn, sizeof(int32_t) * (size_t)n_slots))) return rc;
   if ((rc = ensure(c, c->rowsum, sizeof(RowSummary) * (size_t)n_slots * gr.NT))) return rc;
   if (p->steps_per_symbol <= 0 || p->bins_per_tone <= 0) return fail(c, FT8_E_ARG, "bad oversampling factors");
-  if (p->flags & FT8_FLAG_TOPK) return fail(c, FT8_E_UNSUPPORTED, "FT8_FLAG_TOPK is not implemented yet");
+  if (p->flags != 0) return fail(c, FT8_E_ARG, "ft8_params.flags is reserved and must be 0");
 
   // slot chunks, each an independent STFT -> score/select -> LLR -> BP -> compact chain; chunks
   // alternate over the internal streams so one chunk's BP (FP64 VALU) overlaps the next chunk's

@@ -76,7 +76,6 @@ struct SyncLaunch {
   int N;                   // max candidates
   double min_score;
   int min_score_f64;
-  int flags;
   int32_t* cand;           // [n_slots][N][2]
   double* cand_score;      // [n_slots][N]
   int32_t* cand_count;     // [n_slots]

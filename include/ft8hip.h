@@ -42,9 +42,6 @@ enum ft8_status {
   FT8_E_RANGE = -5        /* a size exceeds a compiled limit (see ft8_limits) */
 };
 
-/* flags */
-#define FT8_FLAG_TOPK 1 /* opt-in true top-k candidate selection (NOT the reference semantics) */
-
 /* Decoder parameters.  Mirrors decode_ft8_message's keyword arguments (ft8_decode.py:288-296);
  * the freq/time masks (ft8_decode.py:322-341) arrive as index ranges computed on the host. */
 typedef struct ft8_params {
@@ -59,7 +56,7 @@ typedef struct ft8_params {
   double min_score;
   int32_t f_lo, f_hi;       /* kept STFT bins [f_lo, f_hi) after f >= 0 and the band mask */
   int32_t t_lo, t_hi;       /* kept frames [t_lo, t_hi) after the time mask */
-  int32_t flags;            /* FT8_FLAG_* */
+  int32_t flags;            /* reserved, must be 0 */
   int32_t reserved;
 } ft8_params;
 
