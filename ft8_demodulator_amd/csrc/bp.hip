@@ -369,6 +369,20 @@ __global__ __launch_bounds__(kWave) void k_llr(BpArgs a) {
   for (int n = lane; n < FT8_LDPC_N; n += kWave) a.llr_out[(int64_t)item * FT8_LDPC_N + n] = c[n];
 }
 
+// Phase boundary inside a sweep.  The workgroup is one wave and the LDS executes a wave's
+// instructions in order, so a later ds_read sees every earlier ds_write of the wave without
+// s_waitcnt / s_barrier; only the compiler must not move LDS accesses across the boundary.
+#ifndef BP_HW_BARRIER
+#define BP_HW_BARRIER 0
+#endif
+__device__ __forceinline__ void sweep_sync() {
+#if BP_HW_BARRIER
+  __syncthreads();
+#else
+  asm volatile("" ::: "memory");
+#endif
+}
+
 // ---- k_bp: persistent waves, one candidate at a time ----------------------------------------------
 // modes: 0 per-slot candidate lists (records carry slot / abs_time / abs_freq / score), 2 plain LLRs
 __global__ __launch_bounds__(kWave, BP_WAVES_PER_EU) void k_bp(BpArgs a) {
@@ -453,7 +467,7 @@ __global__ __launch_bounds__(kWave, BP_WAVES_PER_EU) void k_bp(BpArgs a) {
         *(__attribute__((address_space(3))) double*)(uintptr_t)a1 = __builtin_fmin(__builtin_fmax(-T1 / 2, -4.97), 4.97);
         *(__attribute__((address_space(3))) double*)(uintptr_t)a2 = __builtin_fmin(__builtin_fmax(-T2 / 2, -4.97), 4.97);
       }
-      __syncthreads();
+      sweep_sync();
       // all-zero hard decision -> stop (ldpc_decoder.py:76-78)
       if (any == 0) break;
       // (B) parity check (ldpc_check, ldpc_decoder.py:33-52)
@@ -487,7 +501,7 @@ __global__ __launch_bounds__(kWave, BP_WAVES_PER_EU) void k_bp(BpArgs a) {
       }
 #pragma unroll
       for (int i = 0; i < kEdgeSlots; ++i) L.msg[2 * (lane + kWave * i)] = x[i];
-      __syncthreads();
+      sweep_sync();
       // check -> variable messages: tov = -2 fast_atanh(prod of the other toc of the check, in row
       // order, from 1.0).  The six factor addresses are the row address plus the bytes of the
       // edge's poff word (one SDWA add each); 1.0 * t0 == t0, so the product starts at factor 0.
@@ -523,7 +537,7 @@ __global__ __launch_bounds__(kWave, BP_WAVES_PER_EU) void k_bp(BpArgs a) {
 #pragma unroll
       for (int i = 0; i < kEdgeSlots; ++i) L.msg[2 * (lane + kWave * i)] = x[i];
       passes++;
-      __syncthreads();
+      sweep_sync();
     }
     // bits[] holds the hard decision of the last evaluated sweep
     __syncthreads();
