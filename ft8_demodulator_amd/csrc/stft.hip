@@ -388,6 +388,9 @@ __global__ __launch_bounds__(k38Threads) void k_stft3840(StftArgs a) {
   // (relative error ~15 ulp, far inside the dB tolerance)
   cplx<float> s2 = tw[15 * (t & 15)], s3 = tw[t];
   const bool rec_post = a.f_lo + a.nf_out <= k38P;
+  const bool full = a.f_lo == 0 && a.nf_out == k38P;  // every f >= 0 bin kept (no band mask)
+  // 10 log10(v) = (10 log10 2) log2(v): v_log_f32 on a normal argument (v >= 1e-12)
+  constexpr float kDb = 3.0102999566398119521f;
   cplx<float> p0 = post[min(a.f_lo + t, k38P)];
   const cplx<float> pstep = post[k38Threads];
 
@@ -476,19 +479,40 @@ __global__ __launch_bounds__(k38Threads) void k_stft3840(StftArgs a) {
     __syncthreads();
     // epilogue: real-signal spectrum, power, dB, kept bins
     float* out = outb + ((int64_t)slot * a.nt_out + f) * a.nf_out;
-    cplx<float> pw_k = p0;  // W_3840^k for k = f_lo + i (recurrence over i += 128)
-    for (int i = t; i < a.nf_out; i += k38Threads) {
-      const int k = a.f_lo + i;
-      const int kk = (k <= k38P) ? k : 2 * k38P - k;
-      const cplx<float> A = bufA[kk == k38P ? 0 : kk];
-      const cplx<float> Bc = bufA[kk == 0 ? 0 : k38P - kk];
-      const cplx<float> B = {Bc.x, -Bc.y};
-      const cplx<float> sm = cadd(A, B), df = csub(A, B);
-      const cplx<float> wd = cmul(rec_post ? pw_k : post[kk], df);
-      pw_k = cmul(pw_k, pstep);
-      const cplx<float> X = {0.5f * (sm.x + wd.y), 0.5f * (sm.y - wd.x)};
-      const float pw = (X.x * X.x + X.y * X.y) * scale;
-      out[i] = 10.0f * log10f(1e-12f + pw);
+    if (full) {
+      // all bins [0, P): k and P - k share Z[k], Z[P - k] and, since W_N^(P-k) = -conj(W_N^k),
+      // X[P - k] = conj(s)/2 - i conj(W_N^k d)/2 from the same s = Z[k] + conj Z[P-k],
+      // d = Z[k] - conj Z[P-k]
+      cplx<float> pw_k = p0;  // W_3840^k, k = t + 128 j
+      for (int k = t; k <= k38P / 2; k += k38Threads) {
+        const cplx<float> A = bufA[k];
+        const cplx<float> Bc = bufA[k == 0 ? 0 : k38P - k];
+        const cplx<float> B = {Bc.x, -Bc.y};
+        const cplx<float> sm = cadd(A, B), df = csub(A, B);
+        const cplx<float> wd = cmul(pw_k, df);
+        pw_k = cmul(pw_k, pstep);
+        const float p1 = (0.25f * ((sm.x + wd.y) * (sm.x + wd.y) + (sm.y - wd.x) * (sm.y - wd.x))) * scale;
+        out[k] = kDb * __builtin_amdgcn_logf(1e-12f + p1);
+        if (k != 0 && k != k38P / 2) {
+          const float p2 = (0.25f * ((sm.x - wd.y) * (sm.x - wd.y) + (sm.y + wd.x) * (sm.y + wd.x))) * scale;
+          out[k38P - k] = kDb * __builtin_amdgcn_logf(1e-12f + p2);
+        }
+      }
+    } else {
+      cplx<float> pw_k = p0;  // W_3840^k for k = f_lo + i (recurrence over i += 128)
+      for (int i = t; i < a.nf_out; i += k38Threads) {
+        const int k = a.f_lo + i;
+        const int kk = (k <= k38P) ? k : 2 * k38P - k;
+        const cplx<float> A = bufA[kk == k38P ? 0 : kk];
+        const cplx<float> Bc = bufA[kk == 0 ? 0 : k38P - kk];
+        const cplx<float> B = {Bc.x, -Bc.y};
+        const cplx<float> sm = cadd(A, B), df = csub(A, B);
+        const cplx<float> wd = cmul(rec_post ? pw_k : post[kk], df);
+        pw_k = cmul(pw_k, pstep);
+        const cplx<float> X = {0.5f * (sm.x + wd.y), 0.5f * (sm.y - wd.x)};
+        const float pw = (X.x * X.x + X.y * X.y) * scale;
+        out[i] = kDb * __builtin_amdgcn_logf(1e-12f + pw);
+      }
     }
     // slide the window: pairs r >= 4 become r - 4, the prefetched pairs fill r = 4..7
     if (more) {
