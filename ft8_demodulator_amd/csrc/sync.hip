@@ -213,17 +213,35 @@ __global__ __launch_bounds__(kS2Threads) void k_score2(ScoreArgs a) {
     const float* tb = tile + j * P + 2 * lane;
 #pragma unroll
     for (int m = 0; m < 3; ++m) {
+      const int lo = base + 36 * m;  // block index of the band's first Costas symbol
+      if (lo >= 0 && lo <= nb - 7) {
+        // every symbol of the band and all its neighbours in range: straight-line code, so the
+        // 35 loads issue together (25 differences, in the reference order)
 #pragma unroll
-      for (int k = 0; k < 7; ++k) {
-        const int ba = base + 36 * m + k;
-        if (ba < 0 || ba >= nb) continue;
-        const int tone = kCostasC[k];
-        const float* rp = tb + (m * H + (k + 1) * SPS) * P + tone * BPT;
-        const f32x2 pw = ld2<BPT>(rp);
-        if (tone > 0) { score += pw - ld2<BPT>(rp - BPT); n++; }
-        if (tone < 7) { score += pw - ld2<BPT>(rp + BPT); n++; }
-        if (k > 0 && ba > 0) { score += pw - ld2<BPT>(rp - SPS * P); n++; }
-        if (k < 6 && ba + 1 < nb) { score += pw - ld2<BPT>(rp + SPS * P); n++; }
+        for (int k = 0; k < 7; ++k) {
+          const int tone = kCostasC[k];
+          const float* rp = tb + (m * H + (k + 1) * SPS) * P + tone * BPT;
+          const f32x2 pw = ld2<BPT>(rp);
+          if (tone > 0) score += pw - ld2<BPT>(rp - BPT);
+          if (tone < 7) score += pw - ld2<BPT>(rp + BPT);
+          if (k > 0) score += pw - ld2<BPT>(rp - SPS * P);
+          if (k < 6) score += pw - ld2<BPT>(rp + SPS * P);
+        }
+        n += 25;
+      } else if (lo + 6 >= 0 && lo < nb) {
+        // a band crossing the waterfall's first or last block: the reference's per-term tests
+#pragma unroll
+        for (int k = 0; k < 7; ++k) {
+          const int ba = lo + k;
+          if (ba < 0 || ba >= nb) continue;
+          const int tone = kCostasC[k];
+          const float* rp = tb + (m * H + (k + 1) * SPS) * P + tone * BPT;
+          const f32x2 pw = ld2<BPT>(rp);
+          if (tone > 0) { score += pw - ld2<BPT>(rp - BPT); n++; }
+          if (tone < 7) { score += pw - ld2<BPT>(rp + BPT); n++; }
+          if (k > 0 && ba > 0) { score += pw - ld2<BPT>(rp - SPS * P); n++; }
+          if (k < 6 && ba + 1 < nb) { score += pw - ld2<BPT>(rp + SPS * P); n++; }
+        }
       }
     }
     float res[2];
