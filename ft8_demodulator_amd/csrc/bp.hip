@@ -21,6 +21,7 @@
 // Roofline: the kernel touches < 2 KB of HBM per candidate; it is bound by float64 VALU issue
 // (two IEEE divisions per edge per iteration, ~30 float64 ops per edge per iteration).
 #include "ft8_internal.h"
+#include "heap_replay.h"
 
 namespace ft8 {
 namespace {
@@ -269,7 +270,109 @@ struct BpArgs {
   unsigned* work;
   unsigned long long* stats;  // nullable: [candidates, iterations entered, message passes, converged]
   int slot0;
+  int tie_blocks;             // k_llr's first tie_blocks workgroups run tie_order
+  TieArgs tie;
 };
+
+// The reference heap of one slot whose selected set holds equal scores (k_select left them in
+// scan order, warn bit 3): replay it (heap_replay.h) and write the final candidate order
+// final rank -> select rank, plus the tie flag (warn bit 0).  One wave, beside the LLR workgroups.
+__device__ bool tie_order(const TieArgs& a, int slot) {
+  if (slot >= a.n_slots) return false;
+  const int w = a.warn[slot];
+  if (!(w & 8)) return false;
+  const int lane = threadIdx.x, N = a.N;
+  const int nsel = __builtin_amdgcn_readfirstlane(a.cand_count[slot]);
+  int32_t* t = a.tie + (int64_t)slot * tie_stride(N);
+  const int32_t* push = t;
+  const int32_t* sel = t + N;
+  int32_t* perm = t + 2 * N;
+  int32_t* mi = t + 3 * N;
+  int32_t* mp = t + 4 * N;
+  int32_t* mk = t + 5 * N;
+  const int rec = t[7 * N];
+  const float* sc = a.scores + (int64_t)slot * a.score_stride;
+  unsigned hh[kReplayRegs], hl[kReplayRegs];
+  heap_load(sc, push, nsel, hh, hl);
+  int tie = heap_pushes(nsel, hh, hl);
+  if (rec >= 0) tie |= heap_record(nsel, hh, hl, mono_neg(sc[rec]), (unsigned)rec);
+
+  // members: select ranks whose score equals a neighbour's; record each one's heap position
+  int M = 0;
+  for (int i0 = 0; i0 < nsel; i0 += kWave) {
+    const int i = i0 + lane;
+    unsigned key = 0, idx = 0;
+    bool mem = false;
+    if (i < nsel) {
+      idx = (unsigned)sel[i];
+      key = mono_neg(sc[idx]);
+      mem = (i > 0 && mono_neg(sc[sel[i - 1]]) == key) || (i + 1 < nsel && mono_neg(sc[sel[i + 1]]) == key);
+    }
+    unsigned long long b = __ballot(mem);
+    while (b) {
+      const int l = __ffsll((long long)b) - 1;
+      b &= b - 1;
+      const unsigned sl = rdl(idx, l), kl = rdl(key, l);
+      unsigned P = 0;
+#pragma unroll
+      for (int k = 0; k < kReplayRegs; ++k) {
+        const int pos = 64 * k + lane;
+        const unsigned long long m = __ballot(pos >= 1 && pos <= nsel && hl[k] == sl);
+        if (m) P = 64u * k + (unsigned)(__ffsll((long long)m) - 1);
+      }
+      if (lane == 0) {
+        mi[M] = i0 + l;
+        mp[M] = (int)P;
+        mk[M] = (int)kl;
+      }
+      ++M;
+    }
+  }
+  for (int i = lane; i < nsel; i += kWave) perm[i] = i;
+  __syncthreads();
+  // sorted(key=-score) is stable on heap-array order: within a run of equal scores the final
+  // rank follows the heap position, the select rank the scan index
+  for (int m = lane; m < M; m += kWave) {
+    const int i = mi[m], P = mp[m], K = mk[m];
+    int below_i = 0, below_p = 0;
+    for (int j = 0; j < M; ++j) {
+      if (mk[j] == K) {
+        below_i += mi[j] < i;
+        below_p += mp[j] < P;
+      }
+    }
+    perm[i - below_i + below_p] = i;
+  }
+  if (lane == 0 && tie) a.warn[slot] = w | 1;
+  return true;
+}
+
+// ft8_sync_select: the deferred order applied to the candidate list itself
+__global__ __launch_bounds__(kWave) void k_tie_apply(TieArgs a, int32_t* cand, double* cand_score) {
+  const int slot = blockIdx.x, lane = threadIdx.x, N = a.N;
+  if (!tie_order(a, slot)) return;
+  __syncthreads();
+  const int nsel = a.cand_count[slot];
+  int32_t* t = a.tie + (int64_t)slot * tie_stride(N);
+  const int32_t* perm = t + 2 * N;
+  int32_t* stage = t + 3 * N;  // [nsel] x (time, freq, score lo, score hi)
+  int32_t* cs = cand + (int64_t)slot * N * 2;
+  double* ss = cand_score + (int64_t)slot * N;
+  for (int i = lane; i < nsel; i += kWave) {
+    const int src = perm[i];
+    stage[4 * i] = cs[2 * src];
+    stage[4 * i + 1] = cs[2 * src + 1];
+    const long long v = __double_as_longlong(ss[src]);
+    stage[4 * i + 2] = (int32_t)v;
+    stage[4 * i + 3] = (int32_t)(v >> 32);
+  }
+  __syncthreads();
+  for (int i = lane; i < nsel; i += kWave) {
+    cs[2 * i] = stage[4 * i];
+    cs[2 * i + 1] = stage[4 * i + 1];
+    ss[i] = __longlong_as_double(((long long)stage[4 * i + 3] << 32) | (unsigned)stage[4 * i + 2]);
+  }
+}
 
 // numpy pairwise sum (loops_utils.h.src) of x[0..174): pw(0,80) + pw(80,94), result in lane 0
 __device__ double pairwise174(const double* x, double* part, int lane) {
@@ -329,14 +432,19 @@ __global__ __launch_bounds__(kWave) void k_llr(BpArgs a) {
   __shared__ double sq[FT8_LDPC_N + 2];
   __shared__ double part[16];
   const int lane = threadIdx.x;
-  int item = blockIdx.x;
+  if ((int)blockIdx.x < a.tie_blocks) {
+    tie_order(a.tie, blockIdx.x);
+    return;
+  }
+  const int id = blockIdx.x - a.tie_blocks;  // tie_blocks % 8 == 0 keeps id % 8 == XCD
+  int item = id;
   int slot = 0, at = 0, af = 0;
   if (a.mode == 0) {
     // workgroup id -> (slot, candidate) with slot % 8 == id % 8: all candidates of a slot run on
     // one XCD, so its waterfall rows are fetched into one L2 (round-robin ids would pull every
     // slot into all eight)
-    const int q = blockIdx.x >> 3;
-    slot = (q / a.N) * 8 + (blockIdx.x & 7);
+    const int q = id >> 3;
+    slot = (q / a.N) * 8 + (id & 7);
     const int cidx = q % a.N;
     if (slot >= a.n_slots || cidx >= a.cand_count[slot]) return;
     item = slot * a.N + cidx;
@@ -612,17 +720,25 @@ __global__ __launch_bounds__(kWave, BP_WAVES_PER_EU) void k_bp(BpArgs a) {
 }
 
 // one wave per slot: successes in candidate order -> out[slot][0..cap), counts[slot]
+// (a slot whose order of equal scores was deferred, warn bit 3, is read in its final order)
 __global__ __launch_bounds__(kWave) void k_compact(const ft8_result* res, const int32_t* cand_count,
-                                                   int N, ft8_result* out, int32_t* counts, int cap) {
+                                                   int N, ft8_result* out, int32_t* counts, int cap,
+                                                   const int32_t* warn, const int32_t* tie) {
   const int slot = blockIdx.x, lane = threadIdx.x;
   const int nc = cand_count[slot];
+  const int32_t* perm = (tie && (warn[slot] & 8)) ? tie + (int64_t)slot * tie_stride(N) + 2 * N : nullptr;
+  const ft8_result* rs = res + (int64_t)slot * N;
   int base = 0;
   for (int c0 = 0; c0 < nc; c0 += kWave) {
     const int c = c0 + lane;
-    const bool ok = c < nc && res[(int64_t)slot * N + c].ok;
+    const int src = c < nc ? (perm ? perm[c] : c) : 0;
+    const bool ok = c < nc && rs[src].ok;
     const unsigned long long m = __ballot(ok);
     const int pos = base + __popcll(m & ((1ull << lane) - 1ull));
-    if (ok && pos < cap) out[(int64_t)slot * cap + pos] = res[(int64_t)slot * N + c];
+    if (ok && pos < cap) {
+      out[(int64_t)slot * cap + pos] = rs[src];
+      if (perm) out[(int64_t)slot * cap + pos].cand_index = (uint16_t)c;
+    }
     base += __popcll(m);
   }
   if (lane == 0) counts[slot] = base;
@@ -679,6 +795,8 @@ BpArgs make_args(const BpLaunch& L) {
   a.work = L.work;
   a.stats = L.stats;
   a.slot0 = L.slot0;
+  a.tie = TieArgs{L.n_slots, L.N, L.cand_count, L.warn, L.tie, L.tie_scores, L.tie_score_stride};
+  a.tie_blocks = (L.tie && L.mode == 0) ? (L.n_slots + 7) / 8 * 8 : 0;
   return a;
 }
 
@@ -687,7 +805,7 @@ BpArgs make_args(const BpLaunch& L) {
 hipError_t launch_llr(const BpLaunch& L, hipStream_t s) {
   if (L.n_items <= 0) return hipSuccess;
   BpArgs a = make_args(L);
-  const int64_t grid = L.mode == 0 ? (int64_t)((L.n_slots + 7) / 8) * 8 * L.N : L.n_items;
+  const int64_t grid = a.tie_blocks + (L.mode == 0 ? (int64_t)((L.n_slots + 7) / 8) * 8 * L.N : L.n_items);
   if (L.wf_f64)
     hipLaunchKernelGGL(k_llr<double>, dim3((unsigned)grid), dim3(kWave), 0, s, a);
   else
@@ -706,10 +824,16 @@ hipError_t launch_bp(const BpLaunch& L, hipStream_t s) {
   return hipGetLastError();
 }
 
+hipError_t launch_tie_apply(const TieArgs& a, int32_t* cand, double* cand_score, hipStream_t s) {
+  if (a.n_slots <= 0 || !a.tie) return hipSuccess;
+  hipLaunchKernelGGL(k_tie_apply, dim3(a.n_slots), dim3(kWave), 0, s, a, cand, cand_score);
+  return hipGetLastError();
+}
+
 hipError_t launch_compact(const CompactLaunch& L, hipStream_t s) {
   if (L.n_slots <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_compact, dim3(L.n_slots), dim3(kWave), 0, s, L.res, L.cand_count, L.N, L.out,
-                     L.counts, L.cap);
+                     L.counts, L.cap, L.warn, L.tie);
   return hipGetLastError();
 }
 

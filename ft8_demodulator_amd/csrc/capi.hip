@@ -47,7 +47,7 @@ struct ft8_ctx {
   std::string err;
   std::vector<PlanEntry> plans;
   std::vector<WinEntry> wins;
-  DevBuf wf, scores, cand, cand_score, cand_count, warn, rowsum, res_all, work, stats, llr;
+  DevBuf wf, scores, cand, cand_score, cand_count, warn, rowsum, res_all, work, stats, llr, tie;
   bool timing = false;
   std::vector<TimedLaunch> pending;
   std::vector<hipEvent_t> pool;
@@ -356,7 +356,7 @@ Grid grid_of(int T, int F, int sps, int bpt) {
 
 int sync_select_core(ft8_ctx* c, const void* d_wf, int wf_f64, int n_slots, int T, int F, const ft8_params* p,
                      int32_t* cand, double* cand_score, int32_t* cand_count, void* scores,
-                     int32_t* warn, RowSummary* rowsum, hipStream_t s);
+                     int32_t* warn, RowSummary* rowsum, hipStream_t s, int32_t* tie = nullptr);
 
 int do_sync_select(ft8_ctx* c, const void* d_wf, int wf_f64, int n_slots, int T, int F, const ft8_params* p,
                    int32_t* cand, double* cand_score, int32_t* cand_count, void* d_scores, hipStream_t s) {
@@ -379,15 +379,30 @@ int do_sync_select(ft8_ctx* c, const void* d_wf, int wf_f64, int n_slots, int T,
   }
   if ((rc = ensure(c, c->warn, sizeof(int32_t) * (size_t)n_slots))) return rc;
   if ((rc = ensure(c, c->rowsum, sizeof(RowSummary) * (size_t)n_slots * g.NT))) return rc;
-  return sync_select_core(c, d_wf, wf_f64, n_slots, T, F, p, cand, cand_score, cand_count, scores,
-                          (int32_t*)c->warn.p, (RowSummary*)c->rowsum.p, s);
+  // float32 scores: k_select leaves equal scores in scan order and k_tie_apply replays the
+  // reference heap for the slots that have them (the same code k_llr runs inside decode_batch)
+  int32_t* tie = nullptr;
+  if (!wf_f64) {
+    if ((rc = ensure(c, c->tie, sizeof(int32_t) * (size_t)n_slots * tie_stride(N)))) return rc;
+    tie = (int32_t*)c->tie.p;
+  }
+  int32_t* warn = (int32_t*)c->warn.p;
+  if ((rc = sync_select_core(c, d_wf, wf_f64, n_slots, T, F, p, cand, cand_score, cand_count, scores, warn,
+                             (RowSummary*)c->rowsum.p, s, tie)))
+    return rc;
+  if (tie) {
+    const TieArgs ta{n_slots, N, cand_count, warn, tie, (const float*)scores, (int64_t)g.NT * g.NF};
+    hipError_t e = launch_tie_apply(ta, cand, cand_score, s);
+    if (e != hipSuccess) return hipfail(c, e, "tie launch");
+  }
+  return FT8_OK;
 }
 
 // score + select on caller-provided scratch (scores [n_slots][NT][NF], warn [n_slots],
 // rowsum [n_slots][NT])
 int sync_select_core(ft8_ctx* c, const void* d_wf, int wf_f64, int n_slots, int T, int F, const ft8_params* p,
                      int32_t* cand, double* cand_score, int32_t* cand_count, void* scores,
-                     int32_t* warn, RowSummary* rowsum, hipStream_t s) {
+                     int32_t* warn, RowSummary* rowsum, hipStream_t s, int32_t* tie) {
   const int N = p->max_candidates;
   Grid g = grid_of(T, F, p->steps_per_symbol, p->bins_per_tone);
   SyncLaunch L{};
@@ -410,6 +425,7 @@ int sync_select_core(ft8_ctx* c, const void* d_wf, int wf_f64, int n_slots, int 
   L.cand_count = cand_count;
   L.warn = warn;
   L.rowsum = rowsum;
+  L.tie = tie;
   StageTimer t1(c, 1, s);
   hipError_t e = launch_score(L, s);
   t1.done();
@@ -454,7 +470,7 @@ int ft8_destroy(ft8_ctx* c) {
   {
     DeviceGuard dg(c->device);
     for (auto* b : {&c->wf, &c->scores, &c->cand, &c->cand_score, &c->cand_count, &c->warn, &c->rowsum,
-                    &c->res_all, &c->work, &c->stats, &c->llr})
+                    &c->res_all, &c->work, &c->stats, &c->llr, &c->tie})
       if (b->p) (void)hipFree(b->p);
     for (auto& p : c->plans) {
       if (p.tw) (void)hipFree(p.tw);
@@ -607,6 +623,7 @@ int ft8_decode_batch(ft8_ctx* c, const void* d_samples, int dtype, int64_t n_sam
   if ((rc = ensure(c, c->scores, esz * (size_t)n_slots * gr.NT * gr.NF))) return rc;
   if ((rc = ensure(c, c->warn, sizeof(int32_t) * (size_t)n_slots))) return rc;
   if ((rc = ensure(c, c->rowsum, sizeof(RowSummary) * (size_t)n_slots * gr.NT))) return rc;
+  if (!f64 && (rc = ensure(c, c->tie, sizeof(int32_t) * (size_t)n_slots * tie_stride(N)))) return rc;
   if (p->steps_per_symbol <= 0 || p->bins_per_tone <= 0) return fail(c, FT8_E_ARG, "bad oversampling factors");
   if (p->flags != 0) return fail(c, FT8_E_ARG, "ft8_params.flags is reserved and must be 0");
 
@@ -643,9 +660,13 @@ int ft8_decode_batch(ft8_ctx* c, const void* d_samples, int dtype, int64_t n_sam
     int32_t* cand = (int32_t*)c->cand.p + 2 * (size_t)c0 * N;
     double* cand_score = (double*)c->cand_score.p + (size_t)c0 * N;
     int32_t* cand_count = (int32_t*)c->cand_count.p + c0;
+    // float32 scores: equal scores keep the select order through LLR/BP and are reordered by
+    // k_compact after k_llr's first workgroups replayed the reference heap
+    int32_t* tie = f64 ? nullptr : (int32_t*)c->tie.p + (size_t)c0 * tie_stride(N);
+    int32_t* warn = (int32_t*)c->warn.p + c0;
     if ((rc = sync_select_core(c, wf, f64, ns, T, F, p, cand, cand_score, cand_count,
                                (char*)c->scores.p + esz * (size_t)c0 * gr.NT * gr.NF, (int32_t*)c->warn.p + c0,
-                               (RowSummary*)c->rowsum.p + (size_t)c0 * gr.NT, cs)))
+                               (RowSummary*)c->rowsum.p + (size_t)c0 * gr.NT, cs, tie)))
       return rc;
     BpLaunch B{};
     B.wf = wf;
@@ -670,6 +691,10 @@ int ft8_decode_batch(ft8_ctx* c, const void* d_samples, int dtype, int64_t n_sam
     B.work = (unsigned*)c->work.p + k;
     B.stats = (unsigned long long*)c->stats.p;
     B.grid_waves = n_str > 0 ? c->bp_waves : 4;
+    B.tie = tie;
+    B.warn = warn;
+    B.tie_scores = (const float*)((char*)c->scores.p + esz * (size_t)c0 * gr.NT * gr.NF);
+    B.tie_score_stride = (int64_t)gr.NT * gr.NF;
     StageTimer t6(c, 6, cs);
     e = launch_llr(B, cs);
     t6.done();
@@ -686,6 +711,8 @@ int ft8_decode_batch(ft8_ctx* c, const void* d_samples, int dtype, int64_t n_sam
     C.out = d_out ? d_out + (size_t)c0 * cap : nullptr;
     C.counts = d_counts + c0;
     C.cap = cap;
+    C.warn = warn;
+    C.tie = tie;
     StageTimer t4(c, 4, cs);
     e = launch_compact(C, cs);
     t4.done();

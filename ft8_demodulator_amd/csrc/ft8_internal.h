@@ -80,9 +80,26 @@ struct SyncLaunch {
   double* cand_score;      // [n_slots][N]
   int32_t* cand_count;     // [n_slots]
   int32_t* warn;           // scratch [n_slots] (bit 0: tie reached a heap comparison,
-                           //                    bit 2: equal scores in the selected set)
+                           //                    bit 2: equal scores in the selected set,
+                           //                    bit 3: their order deferred to the LLR kernel)
   RowSummary* rowsum;      // scratch [n_slots][NT]: passing count + max passing score per time row
+  int32_t* tie = nullptr;  // nullable scratch [n_slots][tie_stride(N)]: defer the order of equal
+                           // scores to the LLR kernel (warn bit 3); k_compact applies it
 };
+
+// deferred tie order, per slot: push order [N] | select order [N] | final order [N] |
+// scratch [4N] | last record [1] (heap_replay.h)
+inline __host__ __device__ int64_t tie_stride(int N) { return 7 * (int64_t)N + 2; }
+struct TieArgs {
+  int n_slots, N;
+  const int32_t* cand_count;
+  int32_t* warn;           // bit 3 set by k_select: replay this slot's heap; bit 0 set on a tie
+  int32_t* tie;            // [n_slots][tie_stride(N)]
+  const float* scores;     // float32 score grid [n_slots][score_stride]
+  int64_t score_stride;
+};
+// the deferred order applied to a candidate list ([n_slots][N][2] + [n_slots][N])
+hipError_t launch_tie_apply(const TieArgs& a, int32_t* cand, double* cand_score, hipStream_t s);
 hipError_t launch_score(const SyncLaunch& a, hipStream_t s);
 hipError_t launch_select(const SyncLaunch& a, hipStream_t s);
 
@@ -109,6 +126,12 @@ struct BpLaunch {
   unsigned long long* stats = nullptr;  // [candidates, iterations entered, message passes, converged]
   int slot0 = 0;           // batch index of slot 0 (records carry slot0 + local slot)
   int grid_waves = 4;      // k_bp persistent grid: resident waves per SIMD (<= BP_WAVES_PER_EU)
+  // mode 0, nullable: slots whose order of equal scores k_select deferred (warn bit 3) get it
+  // replayed by k_llr's first workgroups
+  int32_t* tie = nullptr;  // [n_slots][tie_stride(N)]
+  int32_t* warn = nullptr; // [n_slots]
+  const float* tie_scores = nullptr;  // float32 score grid [n_slots][tie_score_stride]
+  int64_t tie_score_stride = 0;
 };
 hipError_t launch_llr(const BpLaunch& a, hipStream_t s);  // k_llr: waterfall -> LLRs
 hipError_t launch_bp(const BpLaunch& a, hipStream_t s);   // k_bp: LLRs -> BP + CRC
@@ -120,6 +143,8 @@ struct CompactLaunch {
   ft8_result* out;         // [n_slots][cap]
   int32_t* counts;
   int cap;
+  const int32_t* warn = nullptr;  // with tie: slots with warn bit 3 are read in the final order
+  const int32_t* tie = nullptr;
 };
 hipError_t launch_compact(const CompactLaunch& a, hipStream_t s);
 

@@ -32,6 +32,7 @@
 // the reference's order depends on heap array positions) replays the reference's N heappushes
 // (one wave wide) to rebuild the heap array and reproduce its stable sort.
 #include "ft8_internal.h"
+#include "heap_replay.h"
 
 namespace ft8 {
 namespace {
@@ -353,6 +354,7 @@ struct SelectArgs {
   int32_t* warn;
   const RowSummary* rowsum;
   int NT;
+  int32_t* tie;  // nullable: defer the order of equal scores (tie_stride(N) ints per slot)
 };
 
 // block-wide exclusive scans over 1024 threads (int sum and double max), via wave shuffles
@@ -639,74 +641,90 @@ __global__ __launch_bounds__(kSelThreads) void k_select(SelectArgs a) {
     if (s_key[i] == s_key[i + 1]) s_flag[0] = 1;
   __syncthreads();
 
+  bool deferred = false;
   if (s_flag[0]) {
     // Exact score ties in the final set: their order is the reference heap's array order, so
-    // rebuild that array.  heapreplace of a record (a strict new maximum, ft8_decode.py:134-137)
-    // moves the min-child path up and sifts the record back to the root, which restores every
-    // other position: the final heap is the heap of the first N pushes with its root replaced by
-    // the last record.  Only the N heappushes need replaying, one wave wide: lane j holds the
-    // j-th ancestor of the new position, a ballot finds how far the item rises.
-    for (int i = threadIdx.x; i < nsel; i += kSelThreads) {
-      s_key[i] = -(double)sc[s_rank[i]];
-      s_sec[i] = s_rank[i];
-    }
-    __syncthreads();
-    if (threadIdx.x < kWave) {
-      const int lane = threadIdx.x;
-      int tie = 0;
-      for (int n = 1; n < nsel; ++n) {
-        const double nk = s_key[n];
-        const int ni = s_sec[n];
-        const int d = 31 - __clz(n + 1);  // ancestors of position n
-        double ak = 0.0;
-        int ai = 0;
-        if (lane < d) {
-          const int pj = ((n + 1) >> (lane + 1)) - 1;
-          ak = s_key[pj];
-          ai = s_sec[pj];
-        }
-        const bool lt = lane < d && (nk < ak || (nk == ak && ni < ai));
-        const int m = __ffsll((long long)~__ballot(lt)) - 1;  // the item passes ancestors 0..m-1
-        if (__any(lane < d && lane <= m && nk == ak)) tie = 1;  // a compared parent with an equal key
-        if (lane < m) {
-          const int dest = lane == 0 ? n : ((n + 1) >> lane) - 1;
-          s_key[dest] = ak;
-          s_sec[dest] = ai;
-        }
-        if (lane == 0) {
-          const int dest = m == 0 ? n : ((n + 1) >> m) - 1;
-          s_key[dest] = nk;
-          s_sec[dest] = ni;
-        }
-        asm volatile("" ::: "memory");  // the next push reads what this one wrote (in-order LDS)
+    // rebuild that array (heap_replay.h): the heap of the first N pushes with its root replaced by
+    // the last record.
+    if constexpr (std::is_same<T, float>::value) deferred = a.tie != nullptr && nsel <= kReplayMax;
+    if (deferred) {
+      // leave the (score, scan index) order and hand the replay to one wave elsewhere: in
+      // decode_batch the first workgroups of k_llr run it beside the LLRs (the set of candidates
+      // is final; only the order of equal scores changes, which k_compact applies), in
+      // ft8_sync_select k_tie_apply runs it and reorders the list
+      int32_t* t = a.tie + (int64_t)slot * tie_stride(a.N);
+      for (int i = threadIdx.x; i < nsel; i += kSelThreads) {
+        t[i] = s_rank[i];
+        t[a.N + i] = s_pay[i];
       }
-      if (lane == 0 && has_rec) {
-        // the records' _siftup compares siblings along the min-child path (same path each time)
-        int c = 1;
-        while (c < nsel) {
-          const int r = c + 1;
-          if (r < nsel) {
-            if (s_key[c] == s_key[r]) tie = 1;
-            const bool cl = s_key[c] < s_key[r] || (s_key[c] == s_key[r] && s_sec[c] < s_sec[r]);
-            if (!cl) c = r;
+      if (threadIdx.x == 0) t[7 * a.N] = has_rec ? s_am_i[0] : -1;
+    } else {
+      for (int i = threadIdx.x; i < nsel; i += kSelThreads) {
+        s_key[i] = -(double)sc[s_rank[i]];
+        s_sec[i] = s_rank[i];
+      }
+      __syncthreads();
+      if (threadIdx.x < kWave) {
+        const int lane = threadIdx.x;
+        int tie = 0;
+        {
+          // float64 scores or N > kReplayMax: lane j holds the j-th ancestor of the new
+          // position, a ballot finds how far the item rises
+          for (int n = 1; n < nsel; ++n) {
+            const double nk = s_key[n];
+            const int ni = s_sec[n];
+            const int d = 31 - __clz(n + 1);  // ancestors of position n
+            double ak = 0.0;
+            int ai = 0;
+            if (lane < d) {
+              const int pj = ((n + 1) >> (lane + 1)) - 1;
+              ak = s_key[pj];
+              ai = s_sec[pj];
+            }
+            const bool lt = lane < d && (nk < ak || (nk == ak && ni < ai));
+            const int m = __ffsll((long long)~__ballot(lt)) - 1;  // the item passes ancestors 0..m-1
+            if (__any(lane < d && lane <= m && nk == ak)) tie = 1;  // a compared parent with an equal key
+            if (lane < m) {
+              const int dest = lane == 0 ? n : ((n + 1) >> lane) - 1;
+              s_key[dest] = ak;
+              s_sec[dest] = ai;
+            }
+            if (lane == 0) {
+              const int dest = m == 0 ? n : ((n + 1) >> m) - 1;
+              s_key[dest] = nk;
+              s_sec[dest] = ni;
+            }
+            asm volatile("" ::: "memory");  // the next push reads what this one wrote (in-order LDS)
           }
-          c = 2 * c + 1;
+          if (lane == 0 && has_rec) {
+            // the records' _siftup compares siblings along the min-child path (same path each time)
+            int c = 1;
+            while (c < nsel) {
+              const int r = c + 1;
+              if (r < nsel) {
+                if (s_key[c] == s_key[r]) tie = 1;
+                const bool cl = s_key[c] < s_key[r] || (s_key[c] == s_key[r] && s_sec[c] < s_sec[r]);
+                if (!cl) c = r;
+              }
+              c = 2 * c + 1;
+            }
+            const int gi = s_am_i[0];
+            s_key[0] = -(double)sc[gi];
+            s_sec[0] = gi;
+          }
         }
-        const int gi = s_am_i[0];
-        s_key[0] = -(double)sc[gi];
-        s_sec[0] = gi;
+        if (lane == 0) s_flag[3] = tie;
       }
-      if (lane == 0) s_flag[3] = tie;
+      __syncthreads();
+      // sorted(key=-score) is stable on heap-array order: secondary key = heap position
+      for (int i = threadIdx.x; i < nsel; i += kSelThreads) { s_pay[i] = s_sec[i]; s_sec[i] = i; }
+      __syncthreads();
+      bitonic(s_key, s_sec, s_pay, nsel);
     }
-    __syncthreads();
-    // sorted(key=-score) is stable on heap-array order: secondary key = heap position
-    for (int i = threadIdx.x; i < nsel; i += kSelThreads) { s_pay[i] = s_sec[i]; s_sec[i] = i; }
-    __syncthreads();
-    bitonic(s_key, s_sec, s_pay, nsel);
   }
   if (threadIdx.x == 0) {
     a.cand_count[slot] = nsel;
-    a.warn[slot] = (s_flag[3] ? 1 : 0) | (s_flag[0] ? 4 : 0);
+    a.warn[slot] = (s_flag[3] ? 1 : 0) | (s_flag[0] ? 4 : 0) | (deferred ? 8 : 0);
   }
   for (int i = threadIdx.x; i < nsel; i += kSelThreads) {
     const int idx = s_pay[i];
@@ -739,6 +757,7 @@ hipError_t launch_select(const SyncLaunch& L, hipStream_t s) {
   a.cand_count = L.cand_count;
   a.warn = L.warn;
   a.rowsum = L.rowsum;
+  a.tie = L.tie;
   a.NT = max(L.NT, 0);
   if (L.wf_f64)
     hipLaunchKernelGGL(k_select<double>, dim3(L.n_slots), dim3(kSelThreads), 0, s, a);

@@ -153,7 +153,8 @@ int ft8_set_pipeline(ft8_ctx* ctx, int32_t chunk_slots, int32_t n_streams, int32
  * bit 0: an exact score tie reached a heap comparison (the reference raises TypeError there,
  *        ftx_types.py:37-47; here ties are ordered by scan index), bit 1: unused (0), bit 2
  *        (informational): the selected set held equal scores, so the heap sequence was replayed
- *        to order them. */
+ *        to order them, bit 3 (informational): that replay ran outside the selection kernel
+ *        (beside the LLRs in ft8_decode_batch). */
 int ft8_select_warnings(ft8_ctx* ctx, int32_t* d_out, int32_t n_slots, void* stream);
 
 /* ---- small device utilities used by the Python mirror of crc.py / ldpc_check ---------------- */

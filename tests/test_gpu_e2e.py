@@ -149,3 +149,39 @@ def test_stream_decoder_matches_resident_decode(gpu):
     files = decode_wave_files(wavs, batch=2)
     for w, r in zip(wavs, files):
         assert key([r]) == key([decode_ft8_from_wave(w)])
+
+
+def test_decode_batch_orders_equal_scores_like_the_reference(gpu, oracle):
+    """ft8_decode_batch leaves equal scores in scan order through LLR/BP (warn bit 3), replays the
+    reference heap in k_llr's first workgroups and lets k_compact apply the order: every record's
+    cand_index, time, frequency and score follow the oracle's heapq order of the same score grid,
+    and the tie flag (bit 0) matches.  The bench workload has such slots."""
+    import torch
+    from ft8_demodulator_amd import FT8Waterfall, SlotDecoder, _device, _lib, synth
+    from ft8_demodulator_amd._pipeline import make_plan
+    x, _ = synth.make_slots(256, 50, seed=100000, device="cuda")
+    dec = SlotDecoder(12000, 2, 2, 300, 2, 20)
+    recs = dec.records(x)
+    w = torch.zeros(256, dtype=torch.int32, device="cuda")
+    dec.ctx.check(_lib.lib().ft8_select_warnings(dec.ctx.handle, _lib.ptr(w), 256, _lib.stream_handle()), "warn")
+    w = w.cpu().numpy()
+    slots = np.nonzero(w & 8)[0]
+    assert len(slots) >= 1 and np.all(w[slots] & 4)
+    plan = make_plan(x.shape[1], 12000, 2, 2)
+    checked = 0
+    for s in slots:
+        wf, _, _ = _device.stft(x[s], 12000, 2, 2, plan.f_lo, plan.f_hi, plan.t_lo, plan.t_hi)
+        mag = np.ascontiguousarray(wf.cpu().numpy().T)
+        grid = oracle.score_grid(mag, 2, 2)
+        t0, _, NF = _device.grid_shape(mag.shape[1], mag.shape[0], 2, 2)
+        idx, sc, tie = oracle.select(grid, 300, 2)
+        exp = [(int(i // NF) + t0, int(i % NF)) for i in idx]
+        cands, _, warn = _device.sync_select(FT8Waterfall(mag=mag, time_osr=2, freq_osr=2), 300, 2)
+        assert [(c[0], c[1]) for c in cands] == exp, s
+        assert bool(w[s] & 1) == tie == bool(warn & 1), s
+        for r in recs[s]:
+            c = int(r["cand_index"])
+            assert (int(r["abs_time"]), int(r["abs_freq"])) == exp[c], (s, c)
+            assert np.float32(r["score"]) == sc[c], (s, c)
+            checked += 1
+    assert checked > 0
