@@ -29,9 +29,10 @@ def waterfall_to_device(wf):
     return t, t.dtype == torch.float64, T, F
 
 
-def sync_params(wf, max_candidates, min_score):
+def sync_params(wf, max_candidates, min_score, flags=0):
     from ._pipeline import min_score_is_f64
     p = _lib.Ft8Params()
+    p.flags = int(flags)
     p.sample_rate = 1
     p.bins_per_tone = int(wf.freq_osr)
     p.steps_per_symbol = int(wf.time_osr)
@@ -50,7 +51,7 @@ def grid_shape(T, F, sps, bpt):
     return t0, NT, NF
 
 
-def sync_select(wf, max_candidates, min_score, want_grid=False):
+def sync_select(wf, max_candidates, min_score, want_grid=False, flags=0):
     """-> (cands [(abs_time, abs_freq, score)], score grid or None, warning flags)."""
     torch = _lib.require_gpu()
     ctx = _lib.context()
@@ -63,7 +64,7 @@ def sync_select(wf, max_candidates, min_score, want_grid=False):
     cs = torch.zeros(max(N, 1), dtype=torch.float64, device=dev)
     cnt = torch.zeros(1, dtype=torch.int32, device=dev)
     grid = torch.empty(max(NT * NF, 1), dtype=d.dtype, device=dev) if want_grid else None
-    p = sync_params(wf, max(N, 1) if want_grid else N, min_score)
+    p = sync_params(wf, max(N, 1) if want_grid else N, min_score, flags)
     rc = _lib.lib().ft8_sync_select(ctx.handle, _lib.ptr(d), int(f64), 1, T, F, ctypes.byref(p),
                                     _lib.ptr(cand), _lib.ptr(cs), _lib.ptr(cnt),
                                     _lib.ptr(grid) if grid is not None else None, _lib.stream_handle())

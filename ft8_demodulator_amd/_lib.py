@@ -16,8 +16,10 @@ LIB_PATH = os.environ.get("FT8HIP_LIB", os.path.join(_HERE, "lib", "libft8hip.so
 
 FT8_F32, FT8_F64, FT8_C64, FT8_C128, FT8_I16 = 0, 1, 2, 3, 4
 FT8_OK, FT8_E_ARG, FT8_E_HIP, FT8_E_UNSUPPORTED, FT8_E_NOMEM, FT8_E_RANGE = 0, -1, -2, -3, -4, -5
-N_STAGES = 7
-STAGE_NAMES = ("stft", "score", "select", "bp", "compact", "decode_batch", "llr")
+FT8_FLAG_TOPK, FT8_FLAG_SUBTRACT = 1, 2
+FT8_TX_PROTOCOL, FT8_TX_REFERENCE = 0, 1
+N_STAGES = 8
+STAGE_NAMES = ("stft", "score", "select", "bp", "compact", "decode_batch", "llr", "subtract")
 
 
 class Ft8Params(ctypes.Structure):
@@ -32,9 +34,17 @@ class Ft8Params(ctypes.Structure):
 # ft8_result (40 bytes) as a NumPy structured dtype
 RESULT_DTYPE = np.dtype({
     "names": ["score", "slot", "abs_time", "abs_freq", "crc_extracted", "crc_calculated",
-              "ldpc_errors", "cand_index", "payload", "ok", "pad"],
+              "ldpc_errors", "cand_index", "payload", "ok", "pass_index"],
     "formats": ["<f8", "<i4", "<i4", "<i4", "<u2", "<u2", "<i2", "<u2", ("u1", (10,)), "u1", "u1"],
     "offsets": [0, 8, 12, 16, 20, 22, 24, 26, 28, 38, 39],
+    "itemsize": 40,
+})
+
+# ft8_tx_signal (40 bytes)
+TX_SIGNAL_DTYPE = np.dtype({
+    "names": ["f0", "amplitude", "phase", "start", "slot", "reserved"],
+    "formats": ["<f8", "<f8", "<f8", "<i8", "<i4", "<i4"],
+    "offsets": [0, 8, 16, 24, 32, 36],
     "itemsize": 40,
 })
 
@@ -82,6 +92,9 @@ def lib():
             "ft8_get_timing": ([vp, vp, vp, ctypes.c_int], ctypes.c_int),
             "ft8_get_counters": ([vp, vp, ctypes.c_int], ctypes.c_int),
             "ft8_set_pipeline": ([vp, i32, i32, i32], ctypes.c_int),
+            "ft8_encode": ([vp, vp, i32, i32, vp, vp, vp, vp], ctypes.c_int),
+            "ft8_synthesize": ([vp, vp, vp, i32, i32, i32, vp, ctypes.c_int, i64, i32, i64, vp], ctypes.c_int),
+            "ft8_subtract": ([vp, vp, ctypes.c_int, vp, i64, i32, i64, P, vp, vp, i32, vp], ctypes.c_int),
         }
         for name, (args, res) in sig.items():
             fn = getattr(L, name)
@@ -95,7 +108,8 @@ def lib():
 EXPORTED_SYMBOLS = (
     "ft8_create", "ft8_destroy", "ft8_last_error", "ft8_abi_version", "ft8_limits", "ft8_geometry",
     "ft8_stft", "ft8_sync_select", "ft8_llr", "ft8_normalize", "ft8_bp", "ft8_decode_batch", "ft8_select_warnings",
-    "ft8_crc14", "ft8_ldpc_check", "ft8_set_timing", "ft8_get_timing", "ft8_get_counters", "ft8_set_pipeline")
+    "ft8_crc14", "ft8_ldpc_check", "ft8_set_timing", "ft8_get_timing", "ft8_get_counters", "ft8_set_pipeline",
+    "ft8_encode", "ft8_synthesize", "ft8_subtract")
 
 
 def limits():

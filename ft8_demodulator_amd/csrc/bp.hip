@@ -682,7 +682,7 @@ __global__ __launch_bounds__(kWave, BP_WAVES_PER_EU) void k_bp(BpArgs a) {
         r.crc_extracted = 0;
         r.crc_calculated = 0;
         r.ok = 0;
-        r.pad = 0;
+        r.pass_index = 0;
         for (int i = 0; i < 10; ++i) r.payload[i] = 0;
         if (min_errors == 0) {
           const uint8_t* a91 = L.a91;

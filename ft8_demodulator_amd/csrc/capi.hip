@@ -48,6 +48,11 @@ struct ft8_ctx {
   std::vector<PlanEntry> plans;
   std::vector<WinEntry> wins;
   DevBuf wf, scores, cand, cand_score, cand_count, warn, rowsum, res_all, work, stats, llr, tie;
+  // FT8_FLAG_SUBTRACT: residual samples, per-record fits, pass-1 / pass-2 records
+  DevBuf residual, sub_est, out1, counts1, out2, counts2;
+  // cumulative GFSK pulse of the transmit chain for one nsps (double and float)
+  int gfsk_nsps = 0;
+  DevBuf gfsk_P, gfsk_Pf;
   bool timing = false;
   std::vector<TimedLaunch> pending;
   std::vector<hipEvent_t> pool;
@@ -354,6 +359,13 @@ Grid grid_of(int T, int F, int sps, int bpt) {
   return g;
 }
 
+int decode_pass(ft8_ctx* c, const void* d_samples, int dtype, int64_t n_samples, int32_t n_slots,
+                int64_t slot_stride, const ft8_params* p, ft8_result* d_out, int32_t* d_counts, int32_t cap,
+                hipStream_t s);
+int subtract_core(ft8_ctx* c, const void* x, int dtype, float* resid, int64_t n_samples, int n_slots,
+                  int64_t x_stride, int64_t r_stride, const ft8_params* p, const ft8_result* res,
+                  const int32_t* counts, int cap, hipStream_t s);
+int gfsk_tables(ft8_ctx* c, int nsps);
 int sync_select_core(ft8_ctx* c, const void* d_wf, int wf_f64, int n_slots, int T, int F, const ft8_params* p,
                      int32_t* cand, double* cand_score, int32_t* cand_count, void* scores,
                      int32_t* warn, RowSummary* rowsum, hipStream_t s, int32_t* tie = nullptr);
@@ -361,7 +373,7 @@ int sync_select_core(ft8_ctx* c, const void* d_wf, int wf_f64, int n_slots, int 
 int do_sync_select(ft8_ctx* c, const void* d_wf, int wf_f64, int n_slots, int T, int F, const ft8_params* p,
                    int32_t* cand, double* cand_score, int32_t* cand_count, void* d_scores, hipStream_t s) {
   if (p->steps_per_symbol <= 0 || p->bins_per_tone <= 0) return fail(c, FT8_E_ARG, "bad oversampling factors");
-  if (p->flags != 0) return fail(c, FT8_E_ARG, "ft8_params.flags is reserved and must be 0");
+  if (p->flags & ~(FT8_FLAG_TOPK | FT8_FLAG_SUBTRACT)) return fail(c, FT8_E_ARG, "unknown bits in ft8_params.flags");
   const int N = p->max_candidates;
   if (N > kMaxCandidates)
     return fail(c, FT8_E_RANGE, "max_candidates > " + std::to_string(kMaxCandidates) + " is not supported");
@@ -426,6 +438,7 @@ int sync_select_core(ft8_ctx* c, const void* d_wf, int wf_f64, int n_slots, int 
   L.warn = warn;
   L.rowsum = rowsum;
   L.tie = tie;
+  L.topk = (p->flags & FT8_FLAG_TOPK) ? 1 : 0;
   StageTimer t1(c, 1, s);
   hipError_t e = launch_score(L, s);
   t1.done();
@@ -435,6 +448,188 @@ int sync_select_core(ft8_ctx* c, const void* d_wf, int wf_f64, int n_slots, int 
   t2.done();
   if (e != hipSuccess) return hipfail(c, e, "select launch");
   return FT8_OK;
+}
+
+int decode_pass(ft8_ctx* c, const void* d_samples, int dtype, int64_t n_samples, int32_t n_slots,
+                int64_t slot_stride, const ft8_params* p, ft8_result* d_out, int32_t* d_counts, int32_t cap,
+                hipStream_t s) {
+  const int T = p->t_hi - p->t_lo, F = p->f_hi - p->f_lo;
+  const bool f64 = is_f64_dtype(dtype);
+  const size_t esz = f64 ? 8 : 4;
+  const int N = p->max_candidates;
+  Grid gr = grid_of(T, F, p->steps_per_symbol, p->bins_per_tone);
+  int rc;
+
+  // slot chunks, each an independent STFT -> score/select -> LLR -> BP -> compact chain; chunks
+  // alternate over the internal streams so one chunk's BP (FP64 VALU) overlaps the next chunk's
+  // STFT / score (LDS, HBM)
+  const int csz = (c->n_streams > 0 && c->chunk_slots > 0) ? c->chunk_slots : n_slots;
+  const int n_chunks = (n_slots + csz - 1) / csz;
+  const int n_str = (c->n_streams > 0 && n_chunks > 1) ? std::min(c->n_streams, n_chunks) : 0;
+  if ((rc = ensure(c, c->work, sizeof(unsigned) * (size_t)std::max(n_chunks, 4)))) return rc;
+  hipError_t e = hipSuccess;
+  if (n_str > 0) {
+    while ((int)c->streams.size() < n_str) {
+      hipStream_t st;
+      if ((e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking)) != hipSuccess) return hipfail(c, e, "stream");
+      c->streams.push_back(st);
+      hipEvent_t ev;
+      if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return hipfail(c, e, "event");
+      c->joins.push_back(ev);
+    }
+    if (!c->fork && (e = hipEventCreateWithFlags(&c->fork, hipEventDisableTiming)) != hipSuccess)
+      return hipfail(c, e, "event");
+    if ((e = hipEventRecord(c->fork, s)) != hipSuccess) return hipfail(c, e, "fork");
+    for (int i = 0; i < n_str; ++i)
+      if ((e = hipStreamWaitEvent(c->streams[i], c->fork, 0)) != hipSuccess) return hipfail(c, e, "fork wait");
+  }
+  const size_t in_esz = dtype == FT8_I16 ? 2 : dtype == FT8_F32 ? 4 : (dtype == FT8_F64 || dtype == FT8_C64) ? 8 : 16;
+  for (int k = 0; k < n_chunks; ++k) {
+    const int c0 = k * csz, ns = std::min(csz, n_slots - c0);
+    hipStream_t cs = n_str > 0 ? c->streams[k % n_str] : s;
+    char* wf = (char*)c->wf.p + esz * (size_t)c0 * T * F;
+    const char* xs = (const char*)d_samples + in_esz * (size_t)c0 * slot_stride;
+    if ((rc = do_stft(c, xs, dtype, n_samples, ns, slot_stride, p, wf, cs))) return rc;
+    int32_t* cand = (int32_t*)c->cand.p + 2 * (size_t)c0 * N;
+    double* cand_score = (double*)c->cand_score.p + (size_t)c0 * N;
+    int32_t* cand_count = (int32_t*)c->cand_count.p + c0;
+    // float32 scores: equal scores keep the select order through LLR/BP and are reordered by
+    // k_compact after k_llr's first workgroups replayed the reference heap
+    int32_t* tie = f64 ? nullptr : (int32_t*)c->tie.p + (size_t)c0 * tie_stride(N);
+    int32_t* warn = (int32_t*)c->warn.p + c0;
+    if ((rc = sync_select_core(c, wf, f64, ns, T, F, p, cand, cand_score, cand_count,
+                               (char*)c->scores.p + esz * (size_t)c0 * gr.NT * gr.NF, (int32_t*)c->warn.p + c0,
+                               (RowSummary*)c->rowsum.p + (size_t)c0 * gr.NT, cs, tie)))
+      return rc;
+    BpLaunch B{};
+    B.wf = wf;
+    B.wf_f64 = f64;
+    B.T = T;
+    B.F = F;
+    B.sps = p->steps_per_symbol;
+    B.bpt = p->bins_per_tone;
+    B.cand = cand;
+    B.cand_score = cand_score;
+    B.cand_count = cand_count;
+    B.N = N;
+    B.n_slots = ns;
+    B.slot0 = c0;
+    B.n_items = ns * N;
+    B.mode = 0;
+    B.normalize = 1;
+    B.max_iterations = p->max_iterations;
+    B.llr_out = (double*)c->llr.p + (size_t)FT8_LDPC_N * c0 * N;
+    B.llr_in = B.llr_out;
+    B.res = (ft8_result*)c->res_all.p + (size_t)c0 * N;
+    B.work = (unsigned*)c->work.p + k;
+    B.stats = (unsigned long long*)c->stats.p;
+    B.grid_waves = n_str > 0 ? c->bp_waves : 4;
+    B.tie = tie;
+    B.warn = warn;
+    B.tie_scores = (const float*)((char*)c->scores.p + esz * (size_t)c0 * gr.NT * gr.NF);
+    B.tie_score_stride = (int64_t)gr.NT * gr.NF;
+    StageTimer t6(c, 6, cs);
+    e = launch_llr(B, cs);
+    t6.done();
+    if (e != hipSuccess) return hipfail(c, e, "llr launch");
+    StageTimer t3(c, 3, cs);
+    e = launch_bp(B, cs);
+    t3.done();
+    if (e != hipSuccess) return hipfail(c, e, "bp launch");
+    CompactLaunch C{};
+    C.res = B.res;
+    C.cand_count = cand_count;
+    C.n_slots = ns;
+    C.N = N;
+    C.out = d_out ? d_out + (size_t)c0 * cap : nullptr;
+    C.counts = d_counts + c0;
+    C.cap = cap;
+    C.warn = warn;
+    C.tie = tie;
+    StageTimer t4(c, 4, cs);
+    e = launch_compact(C, cs);
+    t4.done();
+    if (e != hipSuccess) return hipfail(c, e, "compact launch");
+  }
+  for (int i = 0; i < n_str; ++i) {
+    if ((e = hipEventRecord(c->joins[i], c->streams[i])) != hipSuccess) return hipfail(c, e, "join");
+    if ((e = hipStreamWaitEvent(s, c->joins[i], 0)) != hipSuccess) return hipfail(c, e, "join wait");
+  }
+  return FT8_OK;
+}
+
+// cumulative GFSK frequency pulse P[0 .. 3 nsps] of the transmit chain (tx_device.h), double and
+// float, built once per nsps: p(i) = gauss_window_generator(2.0, (i - 1.5 nsps) / nsps)
+// (modulator.py:20-25, 33-34), P[i + 1] = P[i] + p(i)
+int gfsk_tables(ft8_ctx* c, int nsps) {
+  if (c->gfsk_nsps == nsps && c->gfsk_P.p) return FT8_OK;
+  const int n = 3 * nsps + 1;
+  int rc;
+  if ((rc = ensure(c, c->gfsk_P, sizeof(double) * n))) return rc;
+  if ((rc = ensure(c, c->gfsk_Pf, sizeof(float) * n))) return rc;
+  std::vector<double> P(n);
+  std::vector<float> Pf(n);
+  const double k = M_PI * std::sqrt(2.0 / std::log(2.0)), bt = 2.0;
+  P[0] = 0.0;
+  for (int i = 0; i < 3 * nsps; ++i) {
+    const double t = ((double)i - 1.5 * (double)nsps) / (double)nsps;
+    const double w = 0.5 * (std::erf(k * bt * (t + 0.5)) - std::erf(k * bt * (t - 0.5)));
+    P[i + 1] = P[i] + w;
+  }
+  for (int i = 0; i < n; ++i) Pf[i] = (float)P[i];
+  hipError_t e = hipMemcpy(c->gfsk_P.p, P.data(), sizeof(double) * n, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(c->gfsk_Pf.p, Pf.data(), sizeof(float) * n, hipMemcpyHostToDevice);
+  if (e != hipSuccess) return hipfail(c, e, "gfsk table upload");
+  c->gfsk_nsps = nsps;
+  return FT8_OK;
+}
+
+// decimated samples per symbol of the subtraction's fine sync: 32 when nsps allows, else the
+// largest divisor of nsps in [8, 32]
+int sub_q(int nsps) {
+  for (int q = 32; q >= 8; --q)
+    if (nsps % q == 0) return q;
+  return 0;
+}
+
+int subtract_core(ft8_ctx* c, const void* x, int dtype, float* resid, int64_t n_samples, int n_slots,
+                  int64_t x_stride, int64_t r_stride, const ft8_params* p, const ft8_result* res,
+                  const int32_t* counts, int cap, hipStream_t s) {
+  Geo g;
+  std::string why;
+  int rc = geometry(p->sample_rate, p->bins_per_tone, p->steps_per_symbol, n_samples, &g, &why);
+  if (rc) return fail(c, rc, why);
+  if (dtype != FT8_F32 && dtype != FT8_I16) return fail(c, FT8_E_UNSUPPORTED, "subtraction needs float32 or int16 samples");
+  if (x_stride != r_stride) return fail(c, FT8_E_ARG, "residual and sample strides differ");
+  const int Q = sub_q(g.nperseg);
+  if (Q == 0 || g.nperseg % g.hop != 0)
+    return fail(c, FT8_E_UNSUPPORTED, "subtraction needs nsps with a divisor in [8, 32] and hop | nsps");
+  if ((rc = gfsk_tables(c, g.nperseg))) return rc;
+  if ((rc = ensure(c, c->sub_est, sub_est_bytes() * (size_t)n_slots * (size_t)(cap > 0 ? cap : 1)))) return rc;
+  SubLaunch L{};
+  L.x = x;
+  L.dtype = dtype;
+  L.residual = resid;
+  L.n_samples = n_samples;
+  L.slot_stride = x_stride;
+  L.n_slots = n_slots;
+  L.fs = p->sample_rate;
+  L.nsps = g.nperseg;
+  L.hop = g.hop;
+  L.nfft = g.nfft;
+  L.t_lo = p->t_lo;
+  L.f_lo = p->f_lo;
+  L.res = res;
+  L.counts = counts;
+  L.cap = cap;
+  L.P = (const double*)c->gfsk_P.p;
+  L.Pf = (const float*)c->gfsk_Pf.p;
+  L.est = c->sub_est.p;
+  L.Q = Q;
+  StageTimer tm(c, 7, s);
+  hipError_t e = launch_subtract(L, s);
+  tm.done();
+  return e == hipSuccess ? FT8_OK : hipfail(c, e, "subtract launch");
 }
 
 }  // namespace
@@ -470,7 +665,8 @@ int ft8_destroy(ft8_ctx* c) {
   {
     DeviceGuard dg(c->device);
     for (auto* b : {&c->wf, &c->scores, &c->cand, &c->cand_score, &c->cand_count, &c->warn, &c->rowsum,
-                    &c->res_all, &c->work, &c->stats, &c->llr, &c->tie})
+                    &c->res_all, &c->work, &c->stats, &c->llr, &c->tie, &c->residual, &c->sub_est, &c->out1,
+                    &c->counts1, &c->out2, &c->counts2, &c->gfsk_P, &c->gfsk_Pf})
       if (b->p) (void)hipFree(b->p);
     for (auto& p : c->plans) {
       if (p.tw) (void)hipFree(p.tw);
@@ -625,105 +821,88 @@ int ft8_decode_batch(ft8_ctx* c, const void* d_samples, int dtype, int64_t n_sam
   if ((rc = ensure(c, c->rowsum, sizeof(RowSummary) * (size_t)n_slots * gr.NT))) return rc;
   if (!f64 && (rc = ensure(c, c->tie, sizeof(int32_t) * (size_t)n_slots * tie_stride(N)))) return rc;
   if (p->steps_per_symbol <= 0 || p->bins_per_tone <= 0) return fail(c, FT8_E_ARG, "bad oversampling factors");
-  if (p->flags != 0) return fail(c, FT8_E_ARG, "ft8_params.flags is reserved and must be 0");
-
-  // slot chunks, each an independent STFT -> score/select -> LLR -> BP -> compact chain; chunks
-  // alternate over the internal streams so one chunk's BP (FP64 VALU) overlaps the next chunk's
-  // STFT / score (LDS, HBM)
-  const int csz = (c->n_streams > 0 && c->chunk_slots > 0) ? c->chunk_slots : n_slots;
-  const int n_chunks = (n_slots + csz - 1) / csz;
-  const int n_str = (c->n_streams > 0 && n_chunks > 1) ? std::min(c->n_streams, n_chunks) : 0;
-  if ((rc = ensure(c, c->work, sizeof(unsigned) * (size_t)std::max(n_chunks, 4)))) return rc;
-  hipError_t e = hipSuccess;
-  if (n_str > 0) {
-    while ((int)c->streams.size() < n_str) {
-      hipStream_t st;
-      if ((e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking)) != hipSuccess) return hipfail(c, e, "stream");
-      c->streams.push_back(st);
-      hipEvent_t ev;
-      if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return hipfail(c, e, "event");
-      c->joins.push_back(ev);
-    }
-    if (!c->fork && (e = hipEventCreateWithFlags(&c->fork, hipEventDisableTiming)) != hipSuccess)
-      return hipfail(c, e, "event");
-    if ((e = hipEventRecord(c->fork, s)) != hipSuccess) return hipfail(c, e, "fork");
-    for (int i = 0; i < n_str; ++i)
-      if ((e = hipStreamWaitEvent(c->streams[i], c->fork, 0)) != hipSuccess) return hipfail(c, e, "fork wait");
+  if (p->flags & ~(FT8_FLAG_TOPK | FT8_FLAG_SUBTRACT)) return fail(c, FT8_E_ARG, "unknown bits in ft8_params.flags");
+  if (!(p->flags & FT8_FLAG_SUBTRACT)) {
+    if ((rc = decode_pass(c, d_samples, dtype, n_samples, n_slots, slot_stride, p, d_out, d_counts, cap, s))) return rc;
+    whole.done();
+    return FT8_OK;
   }
-  const size_t in_esz = dtype == FT8_I16 ? 2 : dtype == FT8_F32 ? 4 : (dtype == FT8_F64 || dtype == FT8_C64) ? 8 : 16;
-  for (int k = 0; k < n_chunks; ++k) {
-    const int c0 = k * csz, ns = std::min(csz, n_slots - c0);
-    hipStream_t cs = n_str > 0 ? c->streams[k % n_str] : s;
-    char* wf = (char*)c->wf.p + esz * (size_t)c0 * T * F;
-    const char* xs = (const char*)d_samples + in_esz * (size_t)c0 * slot_stride;
-    if ((rc = do_stft(c, xs, dtype, n_samples, ns, slot_stride, p, wf, cs))) return rc;
-    int32_t* cand = (int32_t*)c->cand.p + 2 * (size_t)c0 * N;
-    double* cand_score = (double*)c->cand_score.p + (size_t)c0 * N;
-    int32_t* cand_count = (int32_t*)c->cand_count.p + c0;
-    // float32 scores: equal scores keep the select order through LLR/BP and are reordered by
-    // k_compact after k_llr's first workgroups replayed the reference heap
-    int32_t* tie = f64 ? nullptr : (int32_t*)c->tie.p + (size_t)c0 * tie_stride(N);
-    int32_t* warn = (int32_t*)c->warn.p + c0;
-    if ((rc = sync_select_core(c, wf, f64, ns, T, F, p, cand, cand_score, cand_count,
-                               (char*)c->scores.p + esz * (size_t)c0 * gr.NT * gr.NF, (int32_t*)c->warn.p + c0,
-                               (RowSummary*)c->rowsum.p + (size_t)c0 * gr.NT, cs, tie)))
-      return rc;
-    BpLaunch B{};
-    B.wf = wf;
-    B.wf_f64 = f64;
-    B.T = T;
-    B.F = F;
-    B.sps = p->steps_per_symbol;
-    B.bpt = p->bins_per_tone;
-    B.cand = cand;
-    B.cand_score = cand_score;
-    B.cand_count = cand_count;
-    B.N = N;
-    B.n_slots = ns;
-    B.slot0 = c0;
-    B.n_items = ns * N;
-    B.mode = 0;
-    B.normalize = 1;
-    B.max_iterations = p->max_iterations;
-    B.llr_out = (double*)c->llr.p + (size_t)FT8_LDPC_N * c0 * N;
-    B.llr_in = B.llr_out;
-    B.res = (ft8_result*)c->res_all.p + (size_t)c0 * N;
-    B.work = (unsigned*)c->work.p + k;
-    B.stats = (unsigned long long*)c->stats.p;
-    B.grid_waves = n_str > 0 ? c->bp_waves : 4;
-    B.tie = tie;
-    B.warn = warn;
-    B.tie_scores = (const float*)((char*)c->scores.p + esz * (size_t)c0 * gr.NT * gr.NF);
-    B.tie_score_stride = (int64_t)gr.NT * gr.NF;
-    StageTimer t6(c, 6, cs);
-    e = launch_llr(B, cs);
-    t6.done();
-    if (e != hipSuccess) return hipfail(c, e, "llr launch");
-    StageTimer t3(c, 3, cs);
-    e = launch_bp(B, cs);
-    t3.done();
-    if (e != hipSuccess) return hipfail(c, e, "bp launch");
-    CompactLaunch C{};
-    C.res = B.res;
-    C.cand_count = cand_count;
-    C.n_slots = ns;
-    C.N = N;
-    C.out = d_out ? d_out + (size_t)c0 * cap : nullptr;
-    C.counts = d_counts + c0;
-    C.cap = cap;
-    C.warn = warn;
-    C.tie = tie;
-    StageTimer t4(c, 4, cs);
-    e = launch_compact(C, cs);
-    t4.done();
-    if (e != hipSuccess) return hipfail(c, e, "compact launch");
-  }
-  for (int i = 0; i < n_str; ++i) {
-    if ((e = hipEventRecord(c->joins[i], c->streams[i])) != hipSuccess) return hipfail(c, e, "join");
-    if ((e = hipStreamWaitEvent(s, c->joins[i], 0)) != hipSuccess) return hipfail(c, e, "join wait");
-  }
+  // ---- FT8_FLAG_SUBTRACT: pass 1 (complete record lists), subtract, pass 2 on the residual, merge
+  if (dtype != FT8_F32 && dtype != FT8_I16)
+    return fail(c, FT8_E_UNSUPPORTED, "FT8_FLAG_SUBTRACT needs float32 or int16 samples");
+  if ((rc = ensure(c, c->out1, sizeof(ft8_result) * (size_t)n_slots * N))) return rc;
+  if ((rc = ensure(c, c->out2, sizeof(ft8_result) * (size_t)n_slots * N))) return rc;
+  if ((rc = ensure(c, c->counts1, sizeof(int32_t) * (size_t)n_slots))) return rc;
+  if ((rc = ensure(c, c->counts2, sizeof(int32_t) * (size_t)n_slots))) return rc;
+  if ((rc = ensure(c, c->residual, sizeof(float) * (size_t)n_slots * n_samples))) return rc;
+  ft8_result* out1 = (ft8_result*)c->out1.p;
+  ft8_result* out2 = (ft8_result*)c->out2.p;
+  int32_t* counts1 = (int32_t*)c->counts1.p;
+  int32_t* counts2 = (int32_t*)c->counts2.p;
+  float* resid = (float*)c->residual.p;
+  if ((rc = decode_pass(c, d_samples, dtype, n_samples, n_slots, slot_stride, p, out1, counts1, N, s))) return rc;
+  if ((rc = subtract_core(c, d_samples, dtype, resid, n_samples, n_slots, slot_stride, n_samples, p, out1, counts1,
+                          N, s)))
+    return rc;
+  if ((rc = decode_pass(c, resid, FT8_F32, n_samples, n_slots, n_samples, p, out2, counts2, N, s))) return rc;
+  hipError_t e = launch_merge_pass(d_out, d_counts, cap, out1, counts1, N, out2, counts2, N, n_slots, s);
+  if (e != hipSuccess) return hipfail(c, e, "merge launch");
   whole.done();
   return FT8_OK;
+}
+
+int ft8_encode(ft8_ctx* c, const uint8_t* d_msg, int32_t msg_bytes, int32_t n, uint8_t* d_a91, uint8_t* d_codeword,
+               uint8_t* d_tones, void* stream) {
+  if (!c || n < 0 || (n > 0 && !d_msg)) return fail(c, FT8_E_ARG, "bad argument");
+  if (msg_bytes != 10 && msg_bytes != 12) return fail(c, FT8_E_ARG, "msg_bytes must be 10 (payload) or 12 (a91)");
+  if (n == 0) return FT8_OK;
+  DeviceGuard dg(c->device);
+  hipError_t e = launch_encode(d_msg, msg_bytes, n, d_a91, d_codeword, d_tones, (hipStream_t)stream);
+  return e == hipSuccess ? FT8_OK : hipfail(c, e, "encode launch");
+}
+
+int ft8_synthesize(ft8_ctx* c, const uint8_t* d_tones, const ft8_tx_signal* d_signals, int32_t n_signals,
+                   int32_t sample_rate, int32_t style, void* d_out, int out_dtype, int64_t n_samples, int32_t n_slots,
+                   int64_t slot_stride, void* stream) {
+  if (!c || n_signals < 0 || n_slots < 0 || n_samples < 0 || sample_rate <= 0) return fail(c, FT8_E_ARG, "bad argument");
+  if (style != FT8_TX_PROTOCOL && style != FT8_TX_REFERENCE) return fail(c, FT8_E_ARG, "unknown ft8_tx_style");
+  if (out_dtype != FT8_F32 && out_dtype != FT8_F64 && out_dtype != FT8_C64 && out_dtype != FT8_C128)
+    return fail(c, FT8_E_ARG, "out_dtype must be FT8_F32, FT8_F64, FT8_C64 or FT8_C128");
+  if (n_signals == 0 || n_slots == 0 || n_samples == 0) return FT8_OK;
+  if (!d_tones || !d_signals || !d_out) return fail(c, FT8_E_ARG, "null argument");
+  if (slot_stride < n_samples && n_slots > 1) return fail(c, FT8_E_ARG, "slot_stride < n_samples");
+  const int nsps = (int)(0.16 * (double)sample_rate);  // modulator.py:31 int(FT8_SYMBOL_TIME_S * fs)
+  if (nsps < 8) return fail(c, FT8_E_ARG, "sample_rate too low (nsps < 8)");
+  DeviceGuard dg(c->device);
+  int rc = gfsk_tables(c, nsps);
+  if (rc) return rc;
+  SynthLaunch L{};
+  L.tones = d_tones;
+  L.sig = d_signals;
+  L.n_sig = n_signals;
+  L.nsps = nsps;
+  L.style = style;
+  L.fs = (double)sample_rate;
+  L.P = (const double*)c->gfsk_P.p;
+  L.out = d_out;
+  L.dtype = out_dtype;
+  L.n_samples = n_samples;
+  L.slot_stride = slot_stride;
+  L.n_slots = n_slots;
+  hipError_t e = launch_synth(L, (hipStream_t)stream);
+  return e == hipSuccess ? FT8_OK : hipfail(c, e, "synthesize launch");
+}
+
+int ft8_subtract(ft8_ctx* c, const void* d_samples, int dtype, float* d_residual, int64_t n_samples, int32_t n_slots,
+                 int64_t slot_stride, const ft8_params* p, const ft8_result* d_res, const int32_t* d_counts, int32_t cap,
+                 void* stream) {
+  if (!c || !p || n_slots < 0 || cap < 0 || n_samples < 0) return fail(c, FT8_E_ARG, "bad argument");
+  if (n_slots == 0 || n_samples == 0) return FT8_OK;
+  if (!d_samples || !d_residual || !d_counts || (cap > 0 && !d_res)) return fail(c, FT8_E_ARG, "null argument");
+  if (slot_stride < n_samples && n_slots > 1) return fail(c, FT8_E_ARG, "slot_stride < n_samples");
+  DeviceGuard dg(c->device);
+  return subtract_core(c, d_samples, dtype, d_residual, n_samples, n_slots, slot_stride, slot_stride, p, d_res,
+                       d_counts, cap, (hipStream_t)stream);
 }
 
 int ft8_set_pipeline(ft8_ctx* c, int32_t chunk_slots, int32_t n_streams, int32_t bp_waves_per_simd) {

@@ -85,6 +85,7 @@ struct SyncLaunch {
   RowSummary* rowsum;      // scratch [n_slots][NT]: passing count + max passing score per time row
   int32_t* tie = nullptr;  // nullable scratch [n_slots][tie_stride(N)]: defer the order of equal
                            // scores to the LLR kernel (warn bit 3); k_compact applies it
+  int topk = 0;            // FT8_FLAG_TOPK: k_topk instead of the reference heap selection
 };
 
 // deferred tie order, per slot: push order [N] | select order [N] | final order [N] |
@@ -147,6 +148,47 @@ struct CompactLaunch {
   const int32_t* tie = nullptr;
 };
 hipError_t launch_compact(const CompactLaunch& a, hipStream_t s);
+
+// ---- transmit chain + subtraction (tx.hip, subtract.hip) -------------------------------------
+struct SynthLaunch {
+  const uint8_t* tones;        // [n_sig][79]
+  const ft8_tx_signal* sig;    // [n_sig], sorted by slot
+  int n_sig;
+  int nsps, style;
+  double fs;
+  const double* P;             // cumulative GFSK pulse [3 nsps + 1]
+  void* out;                   // [n_slots][slot_stride] of dtype (complex: pairs)
+  int dtype;
+  int64_t n_samples, slot_stride;
+  int n_slots;
+};
+hipError_t launch_encode(const uint8_t* msg, int msg_bytes, int n, uint8_t* a91, uint8_t* cw, uint8_t* tones,
+                         hipStream_t s);
+hipError_t launch_synth(const SynthLaunch& a, hipStream_t s);
+
+struct SubLaunch {
+  const void* x;               // samples [n_slots][slot_stride], F32 or I16
+  int dtype;
+  float* residual;             // [n_slots][slot_stride]
+  int64_t n_samples, slot_stride;
+  int n_slots;
+  int fs, nsps, hop, nfft, t_lo, f_lo;
+  const ft8_result* res;       // [n_slots][cap] decoded records
+  const int32_t* counts;       // [n_slots]
+  int cap;
+  const double* P;             // cumulative GFSK pulse [3 nsps + 1] (double)
+  const float* Pf;             // the same in float
+  void* est;                   // scratch [n_slots * cap] SubEst records
+  int Q;                       // decimated samples per symbol (nsps % Q == 0)
+};
+size_t sub_est_bytes();        // sizeof one SubEst record
+hipError_t launch_subtract(const SubLaunch& a, hipStream_t s);
+
+// out[slot] = the pass-1 records out1[slot][0 .. counts1) followed by the pass-2 records
+// out2[slot][0 .. counts2) whose payload no pass-1 record carries (pass_index = 1); counts uncapped
+hipError_t launch_merge_pass(ft8_result* out, int32_t* counts, int cap, const ft8_result* out1,
+                             const int32_t* counts1, int cap1, const ft8_result* out2, const int32_t* counts2,
+                             int cap2, int n_slots, hipStream_t s);
 
 hipError_t launch_crc14(const uint8_t* msg, const int32_t* nbits, int n, uint16_t* crc, hipStream_t s);
 hipError_t launch_ldpc_check(const uint8_t* bits, int n, int32_t* err, hipStream_t s);

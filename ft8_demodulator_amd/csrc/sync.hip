@@ -734,6 +734,133 @@ __global__ __launch_bounds__(kSelThreads) void k_select(SelectArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// FT8_FLAG_TOPK selection (build-defined, outside reference parity): the N highest passing scores,
+// ties in scan order, sorted by score descending.  MSB-first radix select over order-preserving
+// keys (11-bit digits, LDS histogram, early exit once the boundary digit holds exactly the ranks
+// still needed), then one ordered compaction (contiguous scan ranges per thread, so equal scores
+// at the threshold are taken in scan order) and the bitonic sort shared with k_select.
+// ---------------------------------------------------------------------------------------------
+constexpr int kTkBits = 11;
+constexpr int kTkBins = 1 << kTkBits;
+
+template <typename T> struct TkKey;
+template <> struct TkKey<float> {
+  using K = unsigned;
+  static constexpr int kBits = 32;
+  __device__ static K of(float v) {
+    const unsigned u = __float_as_uint(v);
+    return (u >> 31) ? ~u : (u | 0x80000000u);
+  }
+};
+template <> struct TkKey<double> {
+  using K = unsigned long long;
+  static constexpr int kBits = 64;
+  __device__ static K of(double v) { return order_key(v); }
+};
+
+template <typename T>
+__global__ __launch_bounds__(kSelThreads) void k_topk(SelectArgs a) {
+  using K = typename TkKey<T>::K;
+  __shared__ double s_key[kMaxCandidates + 2];
+  __shared__ int s_sec[kMaxCandidates + 2];
+  __shared__ int s_pay[kMaxCandidates + 2];
+  __shared__ unsigned s_hist[kTkBins];
+  __shared__ int s_isum[kSelWaves + 1];
+  __shared__ K s_prefix, s_mask;
+  __shared__ int s_need, s_done;
+
+  const int slot = blockIdx.x;
+  const T* sc = reinterpret_cast<const T*>(a.scores) + (int64_t)slot * a.total;
+  const int N = a.N;
+  const int total = (int)a.total;
+  // passing candidates map to non-zero keys (a key of 0 needs the NaN pattern 0xff..f, excluded)
+  auto key = [&](int i) -> K {
+    const T v = sc[i];
+    return passes(v, a.min_score, a.cmp_f64) ? TkKey<T>::of(v) : (K)0;
+  };
+  if (threadIdx.x == 0) { s_prefix = 0; s_mask = 0; s_need = N; s_done = 0; }
+  __syncthreads();
+  int total_pass = 0;
+  for (int pass = 0;; ++pass) {
+    int shift = TkKey<T>::kBits - kTkBits * (pass + 1), width = kTkBits;
+    if (shift < 0) { width += shift; shift = 0; }
+    const K dmask = ((K)1 << width) - 1;
+    const K prefix = s_prefix, mask = s_mask;
+    for (int b = threadIdx.x; b < kTkBins; b += kSelThreads) s_hist[b] = 0;
+    __syncthreads();
+    for (int i = threadIdx.x; i < total; i += kSelThreads) {
+      const K k = key(i);
+      if (k != 0 && (k & mask) == prefix) atomicAdd(&s_hist[(unsigned)((k >> shift) & dmask)], 1u);
+    }
+    __syncthreads();
+    // suffix counts from the top digit: thread t owns digits 2g, 2g+1 of group g = 1023 - t
+    const int g = kSelThreads - 1 - (int)threadIdx.x;
+    const int hi_c = (int)s_hist[2 * g + 1], lo_c = (int)s_hist[2 * g];
+    int in_prefix;
+    const int above = block_excl_sum(hi_c + lo_c, s_isum, &in_prefix);
+    if (pass == 0) total_pass = in_prefix;
+    const int need = s_need;
+    if (pass == 0 && total_pass <= N) break;  // every passing candidate is selected
+    if (above < need && need <= above + hi_c + lo_c) {
+      const bool top = need <= above + hi_c;
+      const int b = top ? 2 * g + 1 : 2 * g;
+      const int bc = top ? hi_c : lo_c;
+      const int rem = need - (top ? above : above + hi_c);  // ranks still needed inside digit b
+      s_prefix = prefix | ((K)b << shift);
+      s_mask = mask | (dmask << shift);
+      s_need = rem;
+      s_done = (bc == rem || shift == 0) ? 1 : 0;
+    }
+    __syncthreads();
+    if (s_done) break;
+  }
+  const bool take_all = total_pass <= N;
+  const K prefix = s_prefix, mask = s_mask;
+  const int need_eq = s_need;
+  const int nsel = take_all ? total_pass : N;
+  // ordered compaction: thread t scans [t*per, (t+1)*per)
+  const int per = (total + kSelThreads - 1) / kSelThreads;
+  const int i_lo = min(total, (int)threadIdx.x * per), i_hi = min(total, i_lo + per);
+  int n_above = 0, n_eq = 0;
+  for (int i = i_lo; i < i_hi; ++i) {
+    const K k = key(i);
+    if (k == 0) continue;
+    if (take_all || (k & mask) > prefix) n_above++;
+    else if ((k & mask) == prefix) n_eq++;
+  }
+  int tot_above, tot_eq;
+  int pa = block_excl_sum(n_above, s_isum, &tot_above);
+  int pe = block_excl_sum(n_eq, s_isum, &tot_eq);
+  for (int i = i_lo; i < i_hi; ++i) {
+    const K k = key(i);
+    if (k == 0) continue;
+    int pos = -1;
+    if (take_all || (k & mask) > prefix) pos = pa++;
+    else if ((k & mask) == prefix) {
+      if (pe < need_eq) pos = tot_above + pe;
+      pe++;
+    }
+    if (pos >= 0) {
+      s_key[pos] = -(double)sc[i];
+      s_sec[pos] = i;
+      s_pay[pos] = i;
+    }
+  }
+  __syncthreads();
+  bitonic(s_key, s_sec, s_pay, nsel);
+  if (threadIdx.x == 0) {
+    a.cand_count[slot] = nsel;
+    a.warn[slot] = 0;
+  }
+  for (int i = threadIdx.x; i < nsel; i += kSelThreads) {
+    const int idx = s_pay[i];
+    a.cand[((int64_t)slot * a.N + i) * 2 + 0] = a.t0 + idx / a.NF;
+    a.cand[((int64_t)slot * a.N + i) * 2 + 1] = idx % a.NF;
+    a.cand_score[(int64_t)slot * a.N + i] = -s_key[i];
+  }
+}
+
 }  // namespace
 
 hipError_t launch_score(const SyncLaunch& L, hipStream_t s) {
@@ -759,6 +886,13 @@ hipError_t launch_select(const SyncLaunch& L, hipStream_t s) {
   a.rowsum = L.rowsum;
   a.tie = L.tie;
   a.NT = max(L.NT, 0);
+  if (L.topk) {
+    if (L.wf_f64)
+      hipLaunchKernelGGL(k_topk<double>, dim3(L.n_slots), dim3(kSelThreads), 0, s, a);
+    else
+      hipLaunchKernelGGL(k_topk<float>, dim3(L.n_slots), dim3(kSelThreads), 0, s, a);
+    return hipGetLastError();
+  }
   if (L.wf_f64)
     hipLaunchKernelGGL(k_select<double>, dim3(L.n_slots), dim3(kSelThreads), 0, s, a);
   else

@@ -19,7 +19,7 @@ from typing import List, Tuple
 
 import numpy as np
 
-from . import _device
+from . import _device, _lib
 from ._pipeline import SlotDecoder, device_samples, make_plan, records_to_results
 from .crc import compute_crc, extract_crc
 from .ftx_types import FT8Candidate, FT8DecodeStatus, FT8Message, FT8Protocol, FT8Waterfall  # noqa: F401
@@ -54,11 +54,15 @@ def ft8_score_grid(wf: FT8Waterfall) -> np.ndarray:
     return grid
 
 
-def ft8_find_candidates(wf: FT8Waterfall, num_candidates: int, min_score, verbose: bool = False) -> List[FT8Candidate]:
-    """ft8_decode.py:102-149: the reference heap selection, sorted by score descending."""
+def ft8_find_candidates(wf: FT8Waterfall, num_candidates: int, min_score, verbose: bool = False, *,
+                        selection: str = "reference") -> List[FT8Candidate]:
+    """ft8_decode.py:102-149: the reference heap selection, sorted by score descending.
+
+    selection="topk" (build-defined, outside parity) keeps the num_candidates highest passing
+    scores instead of the reference heap's first-N-in-scan-order set."""
     if num_candidates <= 0:
         return []
-    cands, _, _ = _device.sync_select(wf, num_candidates, min_score)
+    cands, _, _ = _device.sync_select(wf, num_candidates, min_score, flags=selection_flags(selection))
     out = [FT8Candidate(waterfall=wf, abs_time=a, abs_freq=b, score=s) for a, b, s in cands]
     if verbose:
         print(f"Number of candidates found: {len(out)}")
@@ -114,14 +118,26 @@ def create_waterfall_from_spectrogram(spectrogram: np.ndarray, time_osr: int, fr
     return FT8Waterfall(mag=spectrogram, time_osr=time_osr, freq_osr=freq_osr)
 
 
+def selection_flags(selection: str = "reference", subtract: bool = False) -> int:
+    """ft8_params.flags for the build-defined options (include/ft8hip.h FT8_FLAG_*)."""
+    if selection not in ("reference", "topk"):
+        raise ValueError("selection must be 'reference' or 'topk'")
+    return (_lib.FT8_FLAG_TOPK if selection == "topk" else 0) | (_lib.FT8_FLAG_SUBTRACT if subtract else 0)
+
+
 def decode_ft8_message(wave_data, sample_rate: int, bins_per_tone: int = 2, steps_per_symbol: int = 2,
                        max_candidates: int = 20, min_score=10, max_iterations: int = 20,
                        freq_min: float = None, freq_max: float = None, time_min: float = None,
-                       time_max: float = None, *, plot: bool = False, verbose: bool = False, device=None):
+                       time_max: float = None, *, plot: bool = False, verbose: bool = False, device=None,
+                       selection: str = "reference", subtract: bool = False):
     """ft8_decode.py:288-394 -> [(FT8Message, FT8DecodeStatus, time_sec, freq_hz, score)].
 
     time_sec = abs_time / sample_rate and freq_hz = abs_freq / bins_per_tone * 6.25 relative to the
-    first kept bin, exactly as the reference reports them (ft8_decode.py:387-388)."""
+    first kept bin, exactly as the reference reports them (ft8_decode.py:387-388).
+
+    Build-defined options (outside reference parity, defaults reproduce the reference):
+    selection="topk" keeps the max_candidates highest scores; subtract=True subtracts the decoded
+    signals and decodes the residual once more, appending new messages (float32 input only)."""
     x, code, wf_f64 = device_samples(wave_data, device)
     if x.dim() != 1:
         raise ValueError("wave_data must be one-dimensional")
@@ -130,7 +146,8 @@ def decode_ft8_message(wave_data, sample_rate: int, bins_per_tone: int = 2, step
     results = []
     if not plan.empty and max_candidates > 0:
         dec = SlotDecoder(sample_rate, bins_per_tone, steps_per_symbol, max_candidates, min_score, max_iterations,
-                          freq_min, freq_max, time_min, time_max, device=x.device)
+                          freq_min, freq_max, time_min, time_max, device=x.device,
+                          flags=selection_flags(selection, subtract))
         recs = dec.records(x.unsqueeze(0), code)[0]
         results = records_to_results(recs, sample_rate, bins_per_tone, wf_f64)
     if plot and not plan.empty:

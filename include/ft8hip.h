@@ -56,9 +56,23 @@ typedef struct ft8_params {
   double min_score;
   int32_t f_lo, f_hi;       /* kept STFT bins [f_lo, f_hi) after f >= 0 and the band mask */
   int32_t t_lo, t_hi;       /* kept frames [t_lo, t_hi) after the time mask */
-  int32_t flags;            /* reserved, must be 0 */
+  int32_t flags;            /* FT8_FLAG_* (0: the reference's behaviour exactly) */
   int32_t reserved;
 } ft8_params;
+
+/* ft8_params.flags.  Both are build-defined extensions OUTSIDE reference parity (the reference
+ * has neither); with flags = 0 every result is the reference's.
+ *   FT8_FLAG_TOPK      candidate selection keeps the max_candidates highest passing scores
+ *                      (ties in scan order), sorted by score descending, instead of reproducing
+ *                      ft8_find_candidates' heap quirk (ft8_decode.py:131-137, which keeps the
+ *                      first N passing candidates in scan order).
+ *   FT8_FLAG_SUBTRACT  ft8_decode_batch runs a second pass: every distinct message decoded in
+ *                      pass 1 is re-modulated (ft8_encode + GFSK), fitted to the slot (time/
+ *                      frequency refinement, per-symbol complex amplitude) and subtracted, and
+ *                      the residual is decoded again.  New messages are appended after the
+ *                      pass-1 results with pass_index = 1.  F32 and I16 samples only. */
+#define FT8_FLAG_TOPK 1
+#define FT8_FLAG_SUBTRACT 2
 
 /* One decoded (or attempted) candidate, 40 bytes, 8-byte aligned. */
 typedef struct ft8_result {
@@ -72,8 +86,26 @@ typedef struct ft8_result {
   uint16_t cand_index;     /* position in the reference candidate order */
   uint8_t payload[10];     /* FT8Message.payload (77 bits, [9] & 0xF8) */
   uint8_t ok;              /* 1: LDPC converged and CRC matched (ft8_decode_candidate True) */
-  uint8_t pad;
+  uint8_t pass_index;      /* 0: decoded from the slot; 1: decoded after subtraction (FT8_FLAG_SUBTRACT) */
 } ft8_result;
+
+/* One transmitted FT8 signal for ft8_synthesize, 40 bytes. */
+typedef struct ft8_tx_signal {
+  double f0;               /* Hz, frequency of tone 0 (the reference's f0 + fc, modulator.py:76-90) */
+  double amplitude;        /* peak amplitude of the real waveform */
+  double phase;            /* radians added to the carrier phase (0: the reference's sin(phi)) */
+  int64_t start;           /* first waveform sample within its slot (may be negative) */
+  int32_t slot;            /* output row; the signal array must be sorted by slot ascending */
+  int32_t reserved;
+} ft8_tx_signal;
+
+/* GFSK timing of ft8_synthesize */
+enum ft8_tx_style {
+  FT8_TX_PROTOCOL = 0,     /* symbol i occupies samples [i nsps, (i+1) nsps); ramp down at the end */
+  FT8_TX_REFERENCE = 1     /* modulator.py exactly: freq_seq read without the one-symbol offset
+                              (modulator.py:64-68, symbols start one symbol late) and its trailing
+                              ramp (modulator.py:72-73) */
+};
 
 typedef struct ft8_ctx ft8_ctx;
 
@@ -165,8 +197,38 @@ int ft8_crc14(ft8_ctx* ctx, const uint8_t* d_msg, const int32_t* d_nbits, int32_
 int ft8_ldpc_check(ft8_ctx* ctx, const uint8_t* d_bits, int32_t n, int32_t* d_errors,
                    void* stream);
 
+/* ---- transmit chain (ft8_generator) and subtract-and-redecode ------------------------------ */
+/* Replaces crc_generator + ldpc_generator + ft8_encode (ft8_generator/crc.py:25-47,
+ * ldpc.py:104-131, encoder.py:15-73).  d_msg[n][msg_bytes]: msg_bytes = 10, a payload (77 bits;
+ * [9] & 0xF8 is applied) whose a91 = crc_generator(payload); msg_bytes = 12, an a91 taken as given
+ * (ldpc_generator's input).  Outputs d_a91[n][12], d_codeword[n][22], d_tones[n][79] (nullable). */
+int ft8_encode(ft8_ctx* ctx, const uint8_t* d_msg, int32_t msg_bytes, int32_t n, uint8_t* d_a91,
+               uint8_t* d_codeword, uint8_t* d_tones, void* stream);
+
+/* Replaces gfsk_modulation_waveform_generator + ft8_modulation_waveform_generator + ft8_generator
+ * (modulator.py:27-90) for a batch: ADDS amplitude * ramp * sin(phi + phase) of every signal to
+ * d_out[slot][start .. start + 79 nsps) (clipped to [0, n_samples)), nsps = int(0.16 fs).
+ * out_dtype FT8_F32 / FT8_F64 (real) or FT8_C64 / FT8_C128 (the complex baseband
+ * amplitude * ramp * (sin - j cos)(phi + phase) of ft8_baseband_generator).  d_tones[n][79];
+ * d_signals sorted by slot.  Signals overlapping in a slot are summed in array order. */
+int ft8_synthesize(ft8_ctx* ctx, const uint8_t* d_tones, const ft8_tx_signal* d_signals, int32_t n_signals,
+                   int32_t sample_rate, int32_t style, void* d_out, int out_dtype, int64_t n_samples,
+                   int32_t n_slots, int64_t slot_stride, void* stream);
+
+/* Subtraction step of FT8_FLAG_SUBTRACT (build-defined; no reference counterpart): for each slot,
+ * every distinct ok message among d_res[slot][0 .. min(d_counts[slot], cap)) (the records of a
+ * ft8_decode_batch with the same params) is re-modulated, its start and tone-0 frequency refined
+ * around the candidate's (abs_time, abs_freq), its complex amplitude fitted per symbol, and the
+ * fitted waveform subtracted: d_residual[slot][n] = x[slot][n] - sum of fitted signals (float32,
+ * row stride slot_stride).  dtype FT8_F32 or FT8_I16 (x / 32767); d_residual may alias F32
+ * d_samples. */
+int ft8_subtract(ft8_ctx* ctx, const void* d_samples, int dtype, float* d_residual, int64_t n_samples,
+                 int32_t n_slots, int64_t slot_stride, const ft8_params* p, const ft8_result* d_res,
+                 const int32_t* d_counts, int32_t cap, void* stream);
+
 /* ---- per-stage device timing (HIP events on the caller's stream) --------------------------- */
-#define FT8_N_STAGES 7 /* 0 stft, 1 score, 2 select, 3 bp, 4 compact, 5 whole decode_batch, 6 llr */
+#define FT8_N_STAGES 8 /* 0 stft, 1 score, 2 select, 3 bp, 4 compact, 5 whole decode_batch, 6 llr,
+                        7 subtract */
 int ft8_set_timing(ft8_ctx* ctx, int enable);
 /* accumulated milliseconds and launch counts per stage since the last reset; synchronises. */
 int ft8_get_timing(ft8_ctx* ctx, double* ms, int64_t* launches, int reset);

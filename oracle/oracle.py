@@ -260,3 +260,93 @@ def decode_ft8_message(wave_data, sample_rate, bins_per_tone=2, steps_per_symbol
                     int(r["abs_time"]) / sample_rate,
                     (int(r["abs_freq"]) / bins_per_tone) * 6.25, score))
     return out
+
+
+# ---- transmit chain (reference src/ft8_tools/ft8_generator) -----------------------------------
+# Plain NumPy restatements; the GFSK sequence follows modulator.py's loops term by term.
+_COSTAS = np.array([3, 1, 4, 0, 6, 5, 2], dtype=np.uint8)   # encoder.py:11
+_GRAY = np.array([0, 1, 3, 2, 5, 6, 4, 7], dtype=np.uint8)  # encoder.py:10
+
+
+def crc_generator(payload10: bytes) -> bytes:
+    """crc.py:25-47: a91 = payload (77 bits) | CRC-14 over 82 bits."""
+    a = bytearray(12)
+    a[:10] = bytes(payload10)[:10]
+    a[9] &= 0xF8
+    c = crc14(bytes(a), 82)
+    a[9] |= c >> 11
+    a[10] = (c >> 3) & 0xFF
+    a[11] = (c << 5) & 0xE0
+    return bytes(a)
+
+
+def tx_itones(payload10: bytes) -> np.ndarray:
+    """encoder.py:15-73 (ft8_encode): payload -> 79 tones."""
+    cw = ldpc_encode(crc_generator(payload10))
+    bits = np.unpackbits(np.frombuffer(cw, dtype=np.uint8))[:174]
+    sym = _GRAY[(bits[0::3] << 2) | (bits[1::3] << 1) | bits[2::3]]
+    return np.concatenate([_COSTAS, sym[:29], _COSTAS, sym[29:], _COSTAS]).astype(np.uint8)
+
+
+def gauss_window(bt: float, t: np.ndarray) -> np.ndarray:
+    """modulator.py:20-25."""
+    from scipy.special import erf
+    k = np.pi * np.sqrt(2 / np.log(2))
+    return 0.5 * (erf(k * bt * (t + 0.5)) - erf(k * bt * (t - 0.5)))
+
+
+def gfsk_freq_seq(itones: np.ndarray, fs: float) -> np.ndarray:
+    """modulator.py:27-50 gfsk_modulation_waveform_generator (same accumulation order)."""
+    nsps = int(0.16 * fs)
+    t = (np.arange(3 * nsps) - 1.5 * nsps) / nsps
+    w = gauss_window(2.0, t)
+    nsym = len(itones)
+    f = np.zeros((nsym + 2) * nsps, dtype=np.float64)
+    for i in range(nsym):
+        f[i * nsps:i * nsps + 3 * nsps] += 6.25 * float(itones[i]) * w
+    f[:2 * nsps] += 6.25 * float(itones[0]) * w[nsps:3 * nsps]
+    f[nsym * nsps:nsym * nsps + 2 * nsps] += 6.25 * float(itones[nsym - 1]) * w[:2 * nsps]
+    return f
+
+
+def gfsk_waveform(itones: np.ndarray, fs: float, f0: float, style: int = 1) -> np.ndarray:
+    """Complex baseband sin(phi) - j cos(phi) with ramps (modulator.py:52-74).  style 1: the
+    reference (freq_seq read from index 0, its trailing ramp); style 0: protocol timing (symbol i
+    at [i nsps, (i+1) nsps), freq_seq read one symbol later) and a falling trailing ramp."""
+    nsps = int(0.16 * fs)
+    nsym = len(itones)
+    L = nsym * nsps
+    f = gfsk_freq_seq(itones, fs)
+    off = 0 if style == 1 else nsps
+    import math
+    dphi = (2 * np.pi * f / fs + 2 * np.pi * f0 / fs)[off:off + L].tolist()
+    phi = np.empty(L, dtype=np.float64)
+    ph, two_pi = 0.0, 2 * np.pi
+    for i in range(L):  # modulator.py:64-68, sequential fmod
+        phi[i] = ph
+        ph = math.fmod(ph + dphi[i], two_pi)
+    y = np.sin(phi) - 1j * np.cos(phi)
+    nramp = nsps // 8
+    i = np.arange(nramp)
+    y[:nramp] *= 0.5 * (1 - np.cos(8 * np.pi * i / nsps))
+    tail = 0.5 * (1 + np.cos(8 * np.pi * i / nsps)) if style == 1 else 0.5 * (1 - np.cos(8 * np.pi * i / nsps))
+    y[L - 1 - i] *= tail
+    return y
+
+
+# ---- FT8_FLAG_TOPK selection (build-defined) --------------------------------------------------
+def select_topk(scores: np.ndarray, N: int, min_score, cmp_f64: bool = False):
+    """The N highest passing scores (ties in scan order), sorted by score descending.  Passing is
+    ft8_find_candidates' test (ft8_decode.py:127): not -inf and score >= min_score, compared in the
+    score dtype unless cmp_f64.  -> (scan_idx, score)."""
+    flat = np.ascontiguousarray(scores.reshape(-1))
+    if cmp_f64 or flat.dtype == np.float64:
+        vals, thr = flat.astype(np.float64), np.float64(min_score)
+    else:
+        vals, thr = flat, flat.dtype.type(min_score)
+    with np.errstate(invalid="ignore"):
+        ok = ~np.isnan(vals) & ~np.isneginf(vals) & (vals >= thr)
+    idx = np.nonzero(ok)[0]
+    order = np.lexsort((idx, -flat[idx].astype(np.float64)))
+    idx = idx[order][:max(int(N), 0)]
+    return idx, flat[idx].astype(np.float64)
