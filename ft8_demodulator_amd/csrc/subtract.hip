@@ -11,7 +11,7 @@
 //   2. baseband: the samples around the candidate are mixed down to the centre of the 8-tone band
 //      and box-car decimated to Q samples per symbol (D = nsps / Q input samples each);
 //   3. fine sync: over start offsets of +-hop/2 (in steps of D samples) and tone-0 offsets of
-//      +-bin/2 (in steps of 6.25/16 Hz) the known tone sequence is correlated symbol by symbol
+//      +-bin/2 (5 points) the known tone sequence is correlated symbol by symbol
 //      (coherent within a symbol, power summed over the 79 symbols); the best point is refined by
 //      a parabola through its neighbours in each direction;
 //   4. the complex amplitude of every symbol is fitted against the refined GFSK waveform
@@ -20,6 +20,8 @@
 //            r(n) Re(A(n) exp(i psi(n))), A linearly interpolated between symbol centres; signals
 //            summed in record order (deterministic).
 // k_merge    one wave per slot: pass-2 records with a payload not decoded in pass 1 are appended.
+#include <algorithm>
+
 #include "tx_device.h"
 
 namespace ft8 {
@@ -28,10 +30,9 @@ namespace {
 constexpr int kSubThreads = 256;
 constexpr int kSubWaves = kSubThreads / kWave;
 constexpr int kMaxQ = 32;
-constexpr int kMaxMg = 2 * kMaxQ + 1;          // margin in decimated samples (sps >= 1)
-constexpr int kMaxZ = tx::kSymbols * kMaxQ + 2 * kMaxMg;
 constexpr int kMaxHyp = 1024;
-constexpr double kFStep = 6.25 / 16.0;         // Hz, tone-0 search step
+constexpr int kMaxT = kMaxQ + 3;                // start offsets searched: 2 ceil(Q / (2 sps)) + 1
+constexpr int kMf = 2;                         // tone-0 search: 2 kMf + 1 points over +-bin/2
 
 struct SubEst {
   int32_t active, pad;
@@ -62,15 +63,17 @@ __device__ __forceinline__ float ramp_f(int n, int L, int nsps) { return tx::gfs
 
 template <typename InT>
 __global__ __launch_bounds__(kSubThreads) void k_sub_est(SubLaunch a) {
-  __shared__ float2 s_z[kMaxZ];
+  // dynamic LDS: the decimated baseband z (phases 2-3), then the float pulse table (phase 4)
+  extern __shared__ float4 s_dyn[];
+  float2* s_z = reinterpret_cast<float2*>(s_dyn);
+  float* s_Pf = reinterpret_cast<float*>(s_dyn);
   __shared__ float s_metric[kMaxHyp];
+  __shared__ float2 s_st[(2 * kMf + 1) * 8];
   __shared__ int s_E[tx::kExt];
   __shared__ int s_PS[tx::kExt + 1];
   __shared__ uint8_t s_tones[80];
   __shared__ float s_ph0[tx::kSymbols + 1];
   __shared__ float2 s_A[tx::kSymbols];
-  __shared__ float s_bv[kSubWaves];
-  __shared__ int s_bi[kSubWaves];
   __shared__ int s_flag;
 
   // records of one slot on one XCD (workgroup id % 8)
@@ -97,8 +100,9 @@ __global__ __launch_bounds__(kSubThreads) void k_sub_est(SubLaunch a) {
     if (threadIdx.x == 0) est->active = 0;
     return;
   }
+  if (threadIdx.x < kWave) tx::encode_tones_wave(r.payload, threadIdx.x, s_tones);
+  __syncthreads();
   if (threadIdx.x == 0) {
-    tx::encode(r.payload, 10, nullptr, nullptr, s_tones);
     int acc = 0;
     for (int k = 0; k < tx::kExt; ++k) {
       const int j = k - 1;
@@ -121,83 +125,123 @@ __global__ __launch_bounds__(kSubThreads) void k_sub_est(SubLaunch a) {
   const double ftone = (double)(a.f_lo + r.abs_freq) * fs / (double)a.nfft;
   const double fmix = ftone + 3.5 * 6.25;
 
-  // ---- 2. mixed-down, box-car decimated baseband z[m], samples [nb + m D, nb + (m + 1) D)
+  // ---- 2. mixed-down, box-car decimated baseband z[m], samples [nb + m D, nb + (m + 1) D).  A
+  // thread owns z[tid + 256 j], j < kZ, and walks their D samples together, kB at a time, so
+  // kZ * kB independent loads are in flight per round trip
   {
+    constexpr int kZ = (tx::kSymbols * kMaxQ + 2 * (kMaxQ / 2 + 2) + kSubThreads - 1) / kSubThreads;
+    constexpr int kB = 2;
     const int64_t nb = s0 - (int64_t)Mg * D;
     float ss, sc;
     sincospif((float)(-2.0 * fmix / fs), &ss, &sc);
     const float2 step = make_float2(sc, ss);
-    for (int m = threadIdx.x; m < Mz; m += kSubThreads) {
-      const int64_t n0 = nb + (int64_t)m * D;
+    float2 wv[kZ], acc[kZ];
+#pragma unroll
+    for (int j = 0; j < kZ; ++j) {
+      const int64_t n0 = nb + (int64_t)(threadIdx.x + j * kSubThreads) * D;
       const double cyc = fmix * (double)n0 / fs;
       float ws, wc;
       sincospif((float)(-2.0 * (cyc - floor(cyc))), &ws, &wc);
-      float2 wv = make_float2(wc, ws), acc = make_float2(0.f, 0.f);
-      for (int i = 0; i < D; ++i) {
-        const int64_t n = n0 + i;
-        if (n >= 0 && n < a.n_samples) {
-          const float v = ld_sample<InT>(x, n);
-          acc.x += v * wv.x;
-          acc.y += v * wv.y;
+      wv[j] = make_float2(wc, ws);
+      acc[j] = make_float2(0.f, 0.f);
+    }
+    for (int i0 = 0; i0 < D; i0 += kB) {
+      float v[kZ][kB];
+#pragma unroll
+      for (int j = 0; j < kZ; ++j) {
+        const int m = threadIdx.x + j * kSubThreads;
+        const int64_t n0 = nb + (int64_t)m * D + i0;
+#pragma unroll
+        for (int u = 0; u < kB; ++u) {
+          const int64_t n = n0 + u;
+          v[j][u] = (m < Mz && i0 + u < D && n >= 0 && n < a.n_samples) ? ld_sample<InT>(x, n) : 0.f;
         }
-        wv = make_float2(wv.x * step.x - wv.y * step.y, wv.x * step.y + wv.y * step.x);
       }
-      s_z[m] = acc;
+#pragma unroll
+      for (int j = 0; j < kZ; ++j) {
+#pragma unroll
+        for (int u = 0; u < kB; ++u) {
+          acc[j].x += v[j][u] * wv[j].x;
+          acc[j].y += v[j][u] * wv[j].y;
+          wv[j] = make_float2(wv[j].x * step.x - wv[j].y * step.y, wv[j].x * step.y + wv[j].y * step.x);
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kZ; ++j) {
+      const int m = threadIdx.x + j * kSubThreads;
+      if (m < Mz) s_z[m] = acc[j];
     }
   }
   __syncthreads();
 
   // ---- 3. fine sync over (start, tone-0) hypotheses
   const double bin = fs / (double)a.nfft;
-  const int Mf = max(1, (int)floor(0.5 * bin / kFStep + 0.5));
+  const int Mf = kMf;
+  const double fstep = 0.5 * bin / kMf;
   const int nT = 2 * Mt + 1, nF = 2 * Mf + 1;
   const int H = min(nT * nF, kMaxHyp);
-  float bv = -1.f;
-  int bi = 0;
-  for (int h = threadIdx.x; h < H; h += kSubThreads) {
-    const int dt = h / nF - Mt, dfi = h % nF - Mf;
-    float2 st[8];
-#pragma unroll
-    for (int t = 0; t < 8; ++t) {
-      const double nu = (double)t * 6.25 + dfi * kFStep - 3.5 * 6.25;  // Hz relative to fmix
-      float s_, c_;
-      sincospif((float)(-2.0 * nu * D / fs), &s_, &c_);
-      st[t] = make_float2(c_, s_);
-    }
-    float metric = 0.f;
-    for (int k = 0; k < tx::kSymbols; ++k) {
-      const float2 stp = st[s_tones[k]];
-      const float2* zp = s_z + Mg + dt + k * Q;
-      float2 wv = make_float2(1.f, 0.f), acc = make_float2(0.f, 0.f);
-      for (int q = 0; q < Q; ++q) {
-        const float2 z = zp[q];
-        acc.x += z.x * wv.x - z.y * wv.y;
-        acc.y += z.x * wv.y + z.y * wv.x;
-        wv = make_float2(wv.x * stp.x - wv.y * stp.y, wv.x * stp.y + wv.y * stp.x);
-      }
-      metric += acc.x * acc.x + acc.y * acc.y;
-    }
-    s_metric[h] = metric;
-    if (metric > bv) { bv = metric; bi = h; }
+  // per-(tone-0 offset, tone) rotation of one decimated sample, staged once
+  if (threadIdx.x < nF * 8) {
+    const int t = threadIdx.x & 7, dfi = (int)threadIdx.x / 8 - Mf;
+    const double nu = (double)t * 6.25 + dfi * fstep - 3.5 * 6.25;  // Hz relative to fmix
+    float s_, c_;
+    sincospif((float)(-2.0 * nu * D / fs), &s_, &c_);
+    s_st[threadIdx.x] = make_float2(c_, s_);
   }
+  __syncthreads();
+  // sliding windows: a wave owns one tone-0 offset at a time and a lane one symbol (k, k + 64);
+  // the lane's coherent window C(dt) = sum_q z[.. + dt + q] w^q slides over every start offset with
+  // one complex update per step, C(dt + 1) = conj(w) (C(dt) - z[dt] + z[dt + Q] w^Q), and the wave
+  // sums |C|^2 over the symbols with a fixed shuffle tree (deterministic)
   {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (int f = wv; f < nF; f += kSubWaves) {
+      float msum[kMaxT];
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const float ov = __shfl_xor(bv, o);
-      const int oi = __shfl_xor(bi, o);
-      if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+      for (int d = 0; d < kMaxT; ++d) msum[d] = 0.f;
+      for (int k = lane; k < tx::kSymbols; k += kWave) {
+        const float2 w = s_st[f * 8 + s_tones[k]];
+        const float2* zp = s_z + Mg - Mt + k * Q;
+        float2 acc = make_float2(0.f, 0.f), wq = make_float2(1.f, 0.f);
+        for (int q = 0; q < Q; ++q) {
+          const float2 z = zp[q];
+          acc.x += z.x * wq.x - z.y * wq.y;
+          acc.y += z.x * wq.y + z.y * wq.x;
+          wq = make_float2(wq.x * w.x - wq.y * w.y, wq.x * w.y + wq.y * w.x);
+        }
+#pragma unroll
+        for (int d = 0; d < kMaxT; ++d) {
+          if (d < nT) {
+            msum[d] += acc.x * acc.x + acc.y * acc.y;
+            if (d + 1 < nT) {
+              const float2 zo = zp[d], zn = zp[d + Q];
+              const float tx_ = acc.x - zo.x + (zn.x * wq.x - zn.y * wq.y);
+              const float ty_ = acc.y - zo.y + (zn.x * wq.y + zn.y * wq.x);
+              acc = make_float2(tx_ * w.x + ty_ * w.y, ty_ * w.x - tx_ * w.y);
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int d = 0; d < kMaxT; ++d) {
+        if (d < nT) {
+          float v = msum[d];
+#pragma unroll
+          for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+          if (lane == 0) s_metric[d * nF + f] = v;
+        }
+      }
     }
-    if (lane == 0) { s_bv[wv] = bv; s_bi[wv] = bi; }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      int b = 0;
-      for (int i = 1; i < kSubWaves; ++i)
-        if (s_bv[i] > s_bv[b] || (s_bv[i] == s_bv[b] && s_bi[i] < s_bi[b])) b = i;
-      s_flag = s_bi[b];
-    }
-    __syncthreads();
   }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int b = 0;
+    for (int h = 1; h < H; ++h)
+      if (s_metric[h] > s_metric[b]) b = h;
+    s_flag = b;
+  }
+  __syncthreads();
   const int hb = s_flag;
   const int dtb = hb / nF - Mt, dfb = hb % nF - Mf;
   auto parab = [](float m_, float m0, float mp) {
@@ -208,9 +252,11 @@ __global__ __launch_bounds__(kSubThreads) void k_sub_est(SubLaunch a) {
   const float ddt = (dtb > -Mt && dtb < Mt) ? parab(s_metric[hb - nF], s_metric[hb], s_metric[hb + nF]) : 0.f;
   const float ddf = (dfb > -Mf && dfb < Mf) ? parab(s_metric[hb - 1], s_metric[hb], s_metric[hb + 1]) : 0.f;
   const int64_t start = s0 + (int64_t)llrintf(((float)dtb + ddt) * (float)D);
-  const double f0 = ftone + ((double)dfb + (double)ddf) * kFStep;
+  const double f0 = ftone + ((double)dfb + (double)ddf) * fstep;
 
-  // ---- phase at every symbol start, exact (double), protocol timing (off = nsps)
+  // ---- phase at every symbol start, exact (double), protocol timing (off = nsps); the float
+  // pulse table replaces z in LDS
+  __syncthreads();
   if (threadIdx.x <= tx::kSymbols) {
     const int k = threadIdx.x;
     const double G0 = tx::gfsk_G<double, double>(s_E, s_PS, a.P, nsps, nsps);
@@ -218,27 +264,42 @@ __global__ __launch_bounds__(kSubThreads) void k_sub_est(SubLaunch a) {
     const double cyc = (f0 * (double)k * nsps + 6.25 * (G - G0)) / fs;
     s_ph0[k] = (float)(cyc - floor(cyc));
   }
+  for (int i = threadIdx.x; i <= 3 * nsps; i += kSubThreads) s_Pf[i] = a.Pf[i];
   __syncthreads();
 
-  // ---- 4. complex amplitude per symbol (one wave per symbol at a time)
+  // ---- 4. complex amplitude per symbol (one wave per symbol at a time; a lane's samples of the
+  // symbol are loaded kPf at a time before they are used)
   {
+    constexpr int kPf = 16;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const float f0r = (float)(f0 / fs), sr = (float)(6.25 / fs);
     for (int k = wv; k < tx::kSymbols; k += kSubWaves) {
       float ax = 0.f, ay = 0.f, rr = 0.f;
       const float ph = s_ph0[k];
-      for (int i = lane; i < nsps; i += kWave) {
-        const int nr = k * nsps + i;
-        const int64_t n = start + nr;
-        if (n < 0 || n >= a.n_samples) continue;
-        const float rp = ramp_f(nr, L, nsps);
-        const float cyc = ph + (float)i * f0r + sr * dG(s_E, a.Pf, nsps, k, i);
-        float sn, cs;
-        sincospif(2.f * (cyc - floorf(cyc)), &sn, &cs);
-        const float v = ld_sample<InT>(x, n) * rp;
-        ax += v * cs;
-        ay -= v * sn;
-        rr += rp * rp;
+      const int64_t nsym = start + (int64_t)k * nsps;
+      const bool inside = nsym >= 0 && nsym + nsps <= a.n_samples;
+      for (int i0 = lane; i0 < nsps; i0 += kPf * kWave) {
+        float v[kPf];
+#pragma unroll
+        for (int u = 0; u < kPf; ++u) {
+          const int i = i0 + u * kWave;
+          const int64_t n = nsym + i;
+          v[u] = (i < nsps && (inside || (n >= 0 && n < a.n_samples))) ? ld_sample<InT>(x, n) : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < kPf; ++u) {
+          const int i = i0 + u * kWave;
+          const int64_t n = nsym + i;
+          if (i >= nsps || !(inside || (n >= 0 && n < a.n_samples))) continue;
+          const float rp = ramp_f(k * nsps + i, L, nsps);
+          const float cyc = ph + (float)i * f0r + sr * dG(s_E, s_Pf, nsps, k, i);
+          const float fr = __builtin_amdgcn_fractf(cyc);  // v_sin / v_cos take revolutions
+          const float sn = __builtin_amdgcn_sinf(fr), cs = __builtin_amdgcn_cosf(fr);
+          const float vr = v[u] * rp;
+          ax += vr * cs;
+          ay -= vr * sn;
+          rr += rp * rp;
+        }
       }
 #pragma unroll
       for (int o = 32; o > 0; o >>= 1) {
@@ -272,7 +333,7 @@ __global__ __launch_bounds__(kSubThreads) void k_sub_est(SubLaunch a) {
   }
 }
 
-constexpr int kApPer = 8;
+constexpr int kApPer = 16;
 constexpr int kApTile = kSubThreads * kApPer;
 
 template <typename InT>
@@ -280,6 +341,8 @@ __global__ __launch_bounds__(kSubThreads) void k_sub_apply(SubLaunch a) {
   __shared__ int s_E[tx::kExt];
   __shared__ float2 s_A[tx::kSymbols];
   __shared__ float s_ph0[tx::kSymbols + 1];
+  extern __shared__ float s_Pf[];  // float pulse table [3 nsps + 1]
+  bool staged = false;
   const int slot = blockIdx.y;
   const int64_t t0 = (int64_t)blockIdx.x * kApTile;
   const int nsps = a.nsps, L = tx::kSymbols * nsps;
@@ -295,6 +358,10 @@ __global__ __launch_bounds__(kSubThreads) void k_sub_apply(SubLaunch a) {
     const int64_t start = e->start;
     if (start >= t0 + kApTile || start + L <= t0) continue;
     __syncthreads();
+    if (!staged) {
+      for (int i = threadIdx.x; i <= 3 * nsps; i += kSubThreads) s_Pf[i] = a.Pf[i];
+      staged = true;
+    }
     if (threadIdx.x < tx::kExt) {
       const int jj = (int)threadIdx.x - 1;
       s_E[threadIdx.x] = e->tones[jj < 0 ? 0 : (jj > tx::kSymbols - 1 ? tx::kSymbols - 1 : jj)];
@@ -310,9 +377,9 @@ __global__ __launch_bounds__(kSubThreads) void k_sub_apply(SubLaunch a) {
       if (nr64 < 0 || nr64 >= L || nabs >= a.n_samples) continue;
       const int nr = (int)nr64;
       const int k = nr / nsps, i = nr - k * nsps;
-      const float cyc = s_ph0[k] + (float)i * f0r + sr * dG(s_E, a.Pf, nsps, k, i);
-      float sn, cs;
-      sincospif(2.f * (cyc - floorf(cyc)), &sn, &cs);
+      const float cyc = s_ph0[k] + (float)i * f0r + sr * dG(s_E, s_Pf, nsps, k, i);
+      const float fr = __builtin_amdgcn_fractf(cyc);  // v_sin / v_cos take revolutions
+      const float sn = __builtin_amdgcn_sinf(fr), cs = __builtin_amdgcn_cosf(fr);
       const float t = ((float)i + 0.5f) / (float)nsps - 0.5f;  // position from the symbol centre
       float2 A;
       if (t < 0.f) {
@@ -380,18 +447,21 @@ hipError_t launch_subtract(const SubLaunch& a, hipStream_t s) {
   if (a.Q <= 0 || a.Q > kMaxQ || a.nsps % a.Q != 0 || a.hop <= 0 || a.nsps % a.hop != 0) return hipErrorInvalidValue;
   if (a.cap > 0) {
     const unsigned grid = (unsigned)(((a.n_slots + 7) / 8) * 8 * (int64_t)a.cap);
+    const size_t mz = (size_t)tx::kSymbols * a.Q + 2 * (a.Q / (2 * (a.nsps / a.hop)) + 2);
+    const size_t lds = std::max(mz * sizeof(float2), (size_t)(3 * a.nsps + 1) * sizeof(float));
     if (a.dtype == FT8_I16)
-      hipLaunchKernelGGL(k_sub_est<int16_t>, dim3(grid), dim3(kSubThreads), 0, s, a);
+      hipLaunchKernelGGL(k_sub_est<int16_t>, dim3(grid), dim3(kSubThreads), lds, s, a);
     else
-      hipLaunchKernelGGL(k_sub_est<float>, dim3(grid), dim3(kSubThreads), 0, s, a);
+      hipLaunchKernelGGL(k_sub_est<float>, dim3(grid), dim3(kSubThreads), lds, s, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
   dim3 g2((unsigned)((a.n_samples + kApTile - 1) / kApTile), (unsigned)a.n_slots);
+  const size_t lds2 = (size_t)(3 * a.nsps + 1) * sizeof(float);
   if (a.dtype == FT8_I16)
-    hipLaunchKernelGGL(k_sub_apply<int16_t>, g2, dim3(kSubThreads), 0, s, a);
+    hipLaunchKernelGGL(k_sub_apply<int16_t>, g2, dim3(kSubThreads), lds2, s, a);
   else
-    hipLaunchKernelGGL(k_sub_apply<float>, g2, dim3(kSubThreads), 0, s, a);
+    hipLaunchKernelGGL(k_sub_apply<float>, g2, dim3(kSubThreads), lds2, s, a);
   return hipGetLastError();
 }
 

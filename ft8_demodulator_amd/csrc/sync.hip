@@ -742,6 +742,7 @@ __global__ __launch_bounds__(kSelThreads) void k_select(SelectArgs a) {
 // at the threshold are taken in scan order) and the bitonic sort shared with k_select.
 // ---------------------------------------------------------------------------------------------
 constexpr int kTkBits = 11;
+constexpr int kTkU = 8;  // grid loads in flight per thread
 constexpr int kTkBins = 1 << kTkBits;
 
 template <typename T> struct TkKey;
@@ -768,7 +769,7 @@ __global__ __launch_bounds__(kSelThreads) void k_topk(SelectArgs a) {
   __shared__ unsigned s_hist[kTkBins];
   __shared__ int s_isum[kSelWaves + 1];
   __shared__ K s_prefix, s_mask;
-  __shared__ int s_need, s_done;
+  __shared__ int s_need, s_done, s_eqcnt, s_cnt;
 
   const int slot = blockIdx.x;
   const T* sc = reinterpret_cast<const T*>(a.scores) + (int64_t)slot * a.total;
@@ -779,7 +780,7 @@ __global__ __launch_bounds__(kSelThreads) void k_topk(SelectArgs a) {
     const T v = sc[i];
     return passes(v, a.min_score, a.cmp_f64) ? TkKey<T>::of(v) : (K)0;
   };
-  if (threadIdx.x == 0) { s_prefix = 0; s_mask = 0; s_need = N; s_done = 0; }
+  if (threadIdx.x == 0) { s_prefix = 0; s_mask = 0; s_need = N; s_done = 0; s_eqcnt = 0; }
   __syncthreads();
   int total_pass = 0;
   for (int pass = 0;; ++pass) {
@@ -789,9 +790,13 @@ __global__ __launch_bounds__(kSelThreads) void k_topk(SelectArgs a) {
     const K prefix = s_prefix, mask = s_mask;
     for (int b = threadIdx.x; b < kTkBins; b += kSelThreads) s_hist[b] = 0;
     __syncthreads();
-    for (int i = threadIdx.x; i < total; i += kSelThreads) {
-      const K k = key(i);
-      if (k != 0 && (k & mask) == prefix) atomicAdd(&s_hist[(unsigned)((k >> shift) & dmask)], 1u);
+    for (int i0 = threadIdx.x; i0 < total; i0 += kTkU * kSelThreads) {
+      K kk[kTkU];
+#pragma unroll
+      for (int u = 0; u < kTkU; ++u) kk[u] = i0 + u * kSelThreads < total ? key(i0 + u * kSelThreads) : (K)0;
+#pragma unroll
+      for (int u = 0; u < kTkU; ++u)
+        if (kk[u] != 0 && (kk[u] & mask) == prefix) atomicAdd(&s_hist[(unsigned)((kk[u] >> shift) & dmask)], 1u);
     }
     __syncthreads();
     // suffix counts from the top digit: thread t owns digits 2g, 2g+1 of group g = 1023 - t
@@ -810,6 +815,7 @@ __global__ __launch_bounds__(kSelThreads) void k_topk(SelectArgs a) {
       s_prefix = prefix | ((K)b << shift);
       s_mask = mask | (dmask << shift);
       s_need = rem;
+      s_eqcnt = bc;
       s_done = (bc == rem || shift == 0) ? 1 : 0;
     }
     __syncthreads();
@@ -819,36 +825,61 @@ __global__ __launch_bounds__(kSelThreads) void k_topk(SelectArgs a) {
   const K prefix = s_prefix, mask = s_mask;
   const int need_eq = s_need;
   const int nsel = take_all ? total_pass : N;
-  // ordered compaction: thread t scans [t*per, (t+1)*per)
-  const int per = (total + kSelThreads - 1) / kSelThreads;
-  const int i_lo = min(total, (int)threadIdx.x * per), i_hi = min(total, i_lo + per);
-  int n_above = 0, n_eq = 0;
-  for (int i = i_lo; i < i_hi; ++i) {
-    const K k = key(i);
-    if (k == 0) continue;
-    if (take_all || (k & mask) > prefix) n_above++;
-    else if ((k & mask) == prefix) n_eq++;
-  }
-  int tot_above, tot_eq;
-  int pa = block_excl_sum(n_above, s_isum, &tot_above);
-  int pe = block_excl_sum(n_eq, s_isum, &tot_eq);
-  for (int i = i_lo; i < i_hi; ++i) {
-    const K k = key(i);
-    if (k == 0) continue;
-    int pos = -1;
-    if (take_all || (k & mask) > prefix) pos = pa++;
-    else if ((k & mask) == prefix) {
-      if (pe < need_eq) pos = tot_above + pe;
-      pe++;
+  int nsort = nsel;
+  if (take_all || (N - need_eq) + s_eqcnt <= kMaxCandidates) {
+    // everything at or above the threshold fits the sort buffer: collect it unordered (coalesced
+    // reads, LDS counter) and let the sort by (-score, scan index) put equal scores in scan order
+    nsort = take_all ? total_pass : (N - need_eq) + s_eqcnt;
+    if (threadIdx.x == 0) s_cnt = 0;
+    __syncthreads();
+    for (int i0 = threadIdx.x; i0 < total; i0 += kTkU * kSelThreads) {
+      K kk[kTkU];
+#pragma unroll
+      for (int u = 0; u < kTkU; ++u) kk[u] = i0 + u * kSelThreads < total ? key(i0 + u * kSelThreads) : (K)0;
+#pragma unroll
+      for (int u = 0; u < kTkU; ++u) {
+        if (kk[u] != 0 && (take_all || (kk[u] & mask) >= prefix)) {
+          const int i = i0 + u * kSelThreads;
+          const int pos = atomicAdd(&s_cnt, 1);
+          s_key[pos] = -(double)sc[i];
+          s_sec[pos] = i;
+          s_pay[pos] = i;
+        }
+      }
     }
-    if (pos >= 0) {
-      s_key[pos] = -(double)sc[i];
-      s_sec[pos] = i;
-      s_pay[pos] = i;
+  } else {
+    // many exactly equal scores at the threshold: ordered compaction, thread t scans
+    // [t*per, (t+1)*per), equal scores taken in scan order
+    const int per = (total + kSelThreads - 1) / kSelThreads;
+    const int i_lo = min(total, (int)threadIdx.x * per), i_hi = min(total, i_lo + per);
+    int n_above = 0, n_eq = 0;
+    for (int i = i_lo; i < i_hi; ++i) {
+      const K k = key(i);
+      if (k == 0) continue;
+      if ((k & mask) > prefix) n_above++;
+      else if ((k & mask) == prefix) n_eq++;
+    }
+    int tot_above, tot_eq;
+    int pa = block_excl_sum(n_above, s_isum, &tot_above);
+    int pe = block_excl_sum(n_eq, s_isum, &tot_eq);
+    for (int i = i_lo; i < i_hi; ++i) {
+      const K k = key(i);
+      if (k == 0) continue;
+      int pos = -1;
+      if ((k & mask) > prefix) pos = pa++;
+      else if ((k & mask) == prefix) {
+        if (pe < need_eq) pos = tot_above + pe;
+        pe++;
+      }
+      if (pos >= 0) {
+        s_key[pos] = -(double)sc[i];
+        s_sec[pos] = i;
+        s_pay[pos] = i;
+      }
     }
   }
   __syncthreads();
-  bitonic(s_key, s_sec, s_pay, nsel);
+  bitonic(s_key, s_sec, s_pay, nsort);
   if (threadIdx.x == 0) {
     a.cand_count[slot] = nsel;
     a.warn[slot] = 0;

@@ -27,7 +27,7 @@ constexpr int kSymbols = 79;
 constexpr int kExt = 81;  // e_{-1} .. e_79
 
 namespace {
-__constant__ uint8_t kGenRowsTx[FT8_LDPC_M * 12] = FT8_GEN_ROWS_INIT;
+__constant__ __attribute__((aligned(16))) uint8_t kGenRowsTx[FT8_LDPC_M * 12] = FT8_GEN_ROWS_INIT;
 __constant__ uint8_t kCostasTx[7] = {3, 1, 4, 0, 6, 5, 2};  // encoder.py:11
 __constant__ uint8_t kGrayTx[8] = {0, 1, 3, 2, 5, 6, 4, 7};   // encoder.py:10
 }  // namespace
@@ -116,6 +116,49 @@ __device__ inline void encode(const uint8_t* msg, int msg_bytes, uint8_t* a91, u
       }
       tones[s < 29 ? 7 + s : 14 + s] = kGrayTx[v];
     }
+  }
+}
+
+// One wave encodes one payload into tones[79] (LDS or global): the 83 parity rows are spread over
+// the lanes (rows l and l + 64) and gathered with two ballots, the 58 data symbols one per lane.
+// Same bits as encode(); used where a single message must be encoded with low latency.
+__device__ inline void encode_tones_wave(const uint8_t* payload, int lane, uint8_t* tones) {
+  uint8_t p[10];
+#pragma unroll
+  for (int i = 0; i < 10; ++i) p[i] = payload[i];
+  p[9] &= 0xF8;
+  const uint64_t m0 = be64(p, 8);
+  const uint64_t m1p = be64(p + 8, 2);
+  const unsigned crc = crc14_words(m0, m1p, 82);
+  const uint64_t m1 = m1p | ((uint64_t)(crc >> 11) << 48) | ((uint64_t)((crc >> 3) & 0xFF) << 40) |
+                      ((uint64_t)((crc << 5) & 0xE0) << 32);
+  auto row_bit = [&](int row) -> bool {
+    const uint32_t* g = reinterpret_cast<const uint32_t*>(kGenRowsTx) + row * 3;
+    const uint64_t g0 = ((uint64_t)__builtin_bswap32(g[0]) << 32) | __builtin_bswap32(g[1]);
+    const uint64_t g1 = (uint64_t)__builtin_bswap32(g[2]) << 32;
+    return ((__popcll(g0 & m0) + __popcll(g1 & m1)) & 1) != 0;
+  };
+  const bool ba = row_bit(lane);
+  const bool bb = lane + 64 < FT8_LDPC_M ? row_bit(lane + 64) : false;
+  const uint64_t par0 = __builtin_bitreverse64(__ballot(ba));  // parity i at bit 63 - i
+  const uint64_t par1 = __builtin_bitreverse64(__ballot(bb));
+  const uint64_t c0 = m0;
+  const uint64_t c1 = (m1 & 0xFFFFFFFF00000000ull) | (par0 >> 27);
+  const uint64_t c2 = (par0 << 37) | (par1 >> 27);
+  if (lane < 7) {
+    tones[lane] = kCostasTx[lane];
+    tones[36 + lane] = kCostasTx[lane];
+    tones[72 + lane] = kCostasTx[lane];
+  }
+  if (lane < 58) {
+    unsigned v = 0;
+#pragma unroll
+    for (int b = 0; b < 3; ++b) {
+      const int i = 3 * lane + b;
+      const uint64_t w = i < 64 ? c0 : (i < 128 ? c1 : c2);
+      v = (v << 1) | (unsigned)((w >> (63 - (i & 63))) & 1ull);
+    }
+    tones[lane < 29 ? 7 + lane : 14 + lane] = kGrayTx[v];
   }
 }
 

@@ -179,6 +179,8 @@ def make_slots(n_slots: int, n_signals: int, fs: int = 12000, snr_db=(-24.0, -10
     torch generator with the same seed for its noise, so slots are reproducible individually.
     """
     N = int(slot_s * fs)
+    if torch.device(device).type == "cuda":
+        return _make_slots_gpu(n_slots, n_signals, fs, snr_db, f0_range, start_range, seed, device, N, noise, seeds)
     out = torch.empty(n_slots, N, dtype=torch.float32, device=device)
     truths = []
     nsps = int(0.16 * fs)
@@ -207,3 +209,35 @@ def make_slots(n_slots: int, n_signals: int, fs: int = 12000, snr_db=(-24.0, -10
         out[b] = acc.to(torch.float32)
         truths.append(SlotTruth(pays, list(f0), list(st), list(snr)))
     return out, truths
+
+
+def _make_slots_gpu(n_slots, n_signals, fs, snr_db, f0_range, start_range, seed, device, N, noise, seeds):
+    """make_slots on the GPU: the same per-slot parameter draws and noise, the waveforms from the
+    HIP transmit chain (ft8_generator.encode_batch / synthesize, protocol timing) in one launch."""
+    from . import _lib
+    from . import ft8_generator as G
+    acc = torch.empty(n_slots, N, dtype=torch.float64, device=device)
+    truths, pays_all, sig_rows = [], [], []
+    for b in range(n_slots):
+        sd = int(seeds[b]) if seeds is not None else seed + b
+        rng = np.random.default_rng(sd)
+        pays = [random_payload(rng) for _ in range(n_signals)]
+        lo, hi = (snr_db, snr_db) if np.isscalar(snr_db) else snr_db
+        snr = rng.uniform(lo, hi, n_signals) if n_signals else np.zeros(0)
+        f0 = rng.uniform(*f0_range, n_signals) if n_signals else np.zeros(0)
+        st = rng.uniform(*start_range, n_signals) if n_signals else np.zeros(0)
+        g = torch.Generator(device=device)
+        g.manual_seed(sd)
+        if noise:
+            acc[b] = torch.randn(N, generator=g, device=device, dtype=torch.float64)
+        else:
+            acc[b].zero_()
+        for i in range(n_signals):
+            pays_all.append(pays[i])
+            sig_rows.append((float(f0[i]), float(np.sqrt(2.0 * 10.0 ** (snr[i] / 10.0))), 0.0, int(st[i] * fs), b, 0))
+        truths.append(SlotTruth(pays, list(f0), list(st), list(snr)))
+    if sig_rows:
+        sig = np.array(sig_rows, dtype=_lib.TX_SIGNAL_DTYPE)
+        _, _, tones = G.encode_batch(np.frombuffer(b"".join(pays_all), dtype=np.uint8).reshape(-1, 10), device=device)
+        G.synthesize(tones, sig, n_slots, N, fs, _lib.FT8_TX_PROTOCOL, out=acc, device=device)
+    return acc.to(torch.float32), truths

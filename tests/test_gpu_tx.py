@@ -259,3 +259,14 @@ def test_subtract_int16_and_batch_consistency(gpu):
     # float64 input is refused with a clear error (subtraction supports float32 / int16)
     with pytest.raises(NotImplementedError):
         SlotDecoder(**kw).records(x.double(), _lib.FT8_F64)
+
+
+def test_make_slots_gpu_matches_cpu(gpu):
+    """The benchmark generator on the GPU (HIP transmit chain) equals the PyTorch CPU restatement."""
+    from ft8_demodulator_amd import synth
+    xg, tg = synth.make_slots(2, 12, seed=77, device="cuda")
+    xc, tc = synth.make_slots(2, 12, seed=77, device="cpu", noise=False)
+    xg0, _ = synth.make_slots(2, 12, seed=77, device="cuda", noise=False)
+    assert [t.payloads for t in tg] == [t.payloads for t in tc]
+    assert float((xg0.cpu() - xc).abs().max()) < 1e-5
+    assert xg.shape == xc.shape and xg.dtype == gpu.float32
