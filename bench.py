@@ -14,6 +14,8 @@ Prints ONE JSON line on rank 0.  Besides the contract fields it carries:
   roofline_hbm  the HBM-bound STFT kernel, GB/s vs the 8 TB/s HBM peak
   stages_ms     per-kernel device time per step (HIP events on the decode stream)
   bp_stress     BASELINE config 4 first pass: 100k LLR vectors x 50 BP iterations, candidates/s (N=1)
+  subtract_redecode  BASELINE config 4 with the subtract-and-redecode second pass: 334 crowded
+                slots x K=300 (top-k), 50 iterations, both passes, candidates/s (N=1)
   h2d_stream    the same slots as int16 PCM in pinned host memory, upload overlapped with decode (N=1)
   cpu_baseline  the oracle port (oracle/, C + scipy) on a bounded sample of the same slots (rank 0, N=1)
 """
@@ -118,6 +120,51 @@ def bp_stress(ctx, dev, n=100000, iters=50, reps=3, sigma=0.85):
                          "unit": "TFLOP/s", "frac": tf / FP64_VECTOR_PEAK_TFLOPS}}
 
 
+def subtract_redecode(dev, n_slots=334, signals=50, iters=50, reps=3):
+    """BASELINE config 4 with the subtract-and-redecode second pass (build-defined):
+    334 crowded slots x K=300 candidates = 100 200 LDPC candidates per pass, 50 BP iterations,
+    top-k candidate selection (FT8_FLAG_TOPK) and FT8_FLAG_SUBTRACT: pass 1, fit + subtract every
+    decoded message, pass 2 on the residual.  candidates/s counts the BP candidates of both passes."""
+    import numpy as np
+    import torch
+    from ft8_demodulator_amd import _lib, synth
+    from ft8_demodulator_amd._pipeline import SlotDecoder
+    x, truths = synth.make_slots(n_slots, signals, fs=12000, snr_db=(-24.0, -10.0), seed=200000, device=dev)
+    dec = SlotDecoder(12000, 2, 2, max_candidates=300, min_score=2, max_iterations=iters, device=dev,
+                      flags=_lib.FT8_FLAG_TOPK | _lib.FT8_FLAG_SUBTRACT)
+    recs = dec.records(x, _lib.FT8_F32)
+    true1 = true2 = false = 0
+    for s in range(n_slots):
+        tr = set(bytes(p) for p in truths[s].payloads)
+        g1 = set(bytes(r["payload"]) for r in recs[s] if r["pass_index"] == 0)
+        g2 = set(bytes(r["payload"]) for r in recs[s] if r["pass_index"] == 1)
+        true1, true2, false = true1 + len(g1 & tr), true2 + len(g2 & tr), false + len((g1 | g2) - tr)
+    ctx = dec.ctx
+    torch.cuda.synchronize()
+    ctx.set_timing(True)
+    ctx.timing(reset=True)
+    ctx.counters(reset=True)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        dec.run(x, _lib.FT8_F32)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    ctx.set_timing(False)
+    tm = ctx.timing(reset=True)
+    cn = ctx.counters(reset=True)
+    del x
+    return {"workload": f"BASELINE config 4 with subtract-and-redecode: {n_slots} crowded slots x K=300 "
+                        f"(top-k selection) = {n_slots * 300} candidates per pass, {iters} BP iterations, "
+                        "pass 1 -> fit and subtract every decoded message -> pass 2 on the residual",
+            "candidates_per_s": cn["candidates"] / dt, "bp_candidates_per_launch": cn["candidates"] / reps,
+            "slots_per_s": n_slots * reps / dt, "ms_per_launch": dt / reps * 1e3,
+            "true_decodes_per_slot_pass1": true1 / n_slots, "true_decodes_per_slot_pass2": true2 / n_slots,
+            "false_decodes": int(false),
+            "stages_ms": {k: v[0] / reps for k, v in tm.items() if v[1] > 0},
+            "data": "synthetic (ft8_demodulator_amd.synth, seeds 200000..), parity unpinned: the reference "
+                    "has no second pass"}
+
+
 def h2d_stream(x, steps, kw):
     """Slots handed over as 16-bit PCM in pinned host memory (the WAV ingestion path): the upload of
     batch k+1 on a copy stream overlaps the decode of batch k.  PCIe-inclusive slots/s -- reported
@@ -153,6 +200,7 @@ def main():
     ap.add_argument("--cpu-slots", type=int, default=256)
     ap.add_argument("--no-bp-stress", action="store_true", help="skip the config-4 BP stress leg")
     ap.add_argument("--no-h2d", action="store_true", help="skip the PCIe-inclusive streaming leg")
+    ap.add_argument("--no-subtract", action="store_true", help="skip the config-4 subtract-and-redecode leg")
     args = ap.parse_args()
 
     import torch
@@ -241,6 +289,9 @@ def main():
     stream = None
     if world == 1 and not args.no_h2d:
         stream = h2d_stream(x, max(3, min(args.steps, 10)), kw)
+    sub = None
+    if world == 1 and not args.no_subtract:
+        sub = subtract_redecode(dev)
 
     # HBM bytes per launch from the committed rocprofv3 PMC summary (tools/pmc_traffic.py; FETCH_SIZE
     # and WRITE_SIZE passes of the same 256-slot workload), or null when it is absent
@@ -287,6 +338,7 @@ def main():
         "stages_ms": stage_ms,
         "bp_stress": stress,
         "h2d_stream": stream,
+        "subtract_redecode": sub,
         "cpu_baseline": cpu,
     }
     if rank == 0:
