@@ -211,7 +211,7 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     kw = dict(max_candidates=300, min_score=2, max_iterations=20)
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if rank == 0 and world == 1 and not args.no_cpu and args.cpu_slots > 0:
         procs = max(1, min(16, len(os.sched_getaffinity(0))))
         cpu = cpu_baseline(kw, min(args.cpu_slots, args.slots), procs, 100000, args.signals)
     torch.cuda.set_device(local)
