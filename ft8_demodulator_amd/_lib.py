@@ -18,8 +18,13 @@ FT8_F32, FT8_F64, FT8_C64, FT8_C128, FT8_I16 = 0, 1, 2, 3, 4
 FT8_OK, FT8_E_ARG, FT8_E_HIP, FT8_E_UNSUPPORTED, FT8_E_NOMEM, FT8_E_RANGE = 0, -1, -2, -3, -4, -5
 FT8_FLAG_TOPK, FT8_FLAG_SUBTRACT = 1, 2
 FT8_TX_PROTOCOL, FT8_TX_REFERENCE = 0, 1
-N_STAGES = 8
-STAGE_NAMES = ("stft", "score", "select", "bp", "compact", "decode_batch", "llr", "subtract")
+N_STAGES = 11
+STAGE_NAMES = ("stft", "score", "select", "bp", "compact", "decode_batch", "llr", "subtract",
+               "drift_stft_argmax", "drift_fit", "drift_derotate")
+# ft8_drift_status
+(FT8_DRIFT_PENDING, FT8_DRIFT_NO_SEGMENT, FT8_DRIFT_LINEAR, FT8_DRIFT_FEW_POINTS, FT8_DRIFT_DEGREE,
+ FT8_DRIFT_FULL, FT8_DRIFT_UNDERDETERMINED) = range(7)
+FT8_DRIFT_VALUE_ERROR = -1
 
 
 class Ft8Params(ctypes.Structure):
@@ -30,6 +35,23 @@ class Ft8Params(ctypes.Structure):
                 ("t_lo", ctypes.c_int32), ("t_hi", ctypes.c_int32), ("flags", ctypes.c_int32),
                 ("reserved", ctypes.c_int32)]
 
+
+class Ft8DriftParams(ctypes.Structure):
+    _fields_ = [("sample_rate", ctypes.c_double), ("sym_bin", ctypes.c_double), ("sym_t", ctypes.c_double),
+                ("max_variance_factor", ctypes.c_double), ("bins_per_tone", ctypes.c_int32),
+                ("steps_per_symbol", ctypes.c_int32), ("nsync_sym", ctypes.c_int32), ("ndata_sym", ctypes.c_int32),
+                ("window_size_factor", ctypes.c_int32), ("fit_middle_percent", ctypes.c_int32),
+                ("poly_degree", ctypes.c_int32), ("precise_sync", ctypes.c_int32)]
+
+
+# ft8_drift_result (72 bytes)
+DRIFT_RESULT_DTYPE = np.dtype({
+    "names": ["rate_per_sample", "rate1", "coef", "intercept", "status", "n_segments", "seg_start", "seg_end",
+              "sync_idx", "n_points"],
+    "formats": ["<f8", "<f8", ("<f8", (3,)), "<f8", "<i4", "<i4", "<i4", "<i4", "<i4", "<i4"],
+    "offsets": [0, 8, 16, 40, 48, 52, 56, 60, 64, 68],
+    "itemsize": 72,
+})
 
 # ft8_result (40 bytes) as a NumPy structured dtype
 RESULT_DTYPE = np.dtype({
@@ -72,6 +94,7 @@ def lib():
         L = ctypes.CDLL(LIB_PATH)
         vp, i32, i64, dbl = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_double
         P = ctypes.POINTER(Ft8Params)
+        DP = ctypes.POINTER(Ft8DriftParams)
         sig = {
             "ft8_create": ([ctypes.c_int, ctypes.POINTER(vp)], ctypes.c_int),
             "ft8_destroy": ([vp], ctypes.c_int),
@@ -95,6 +118,9 @@ def lib():
             "ft8_encode": ([vp, vp, i32, i32, vp, vp, vp, vp], ctypes.c_int),
             "ft8_synthesize": ([vp, vp, vp, i32, i32, i32, vp, ctypes.c_int, i64, i32, i64, vp], ctypes.c_int),
             "ft8_subtract": ([vp, vp, ctypes.c_int, vp, i64, i32, i64, P, vp, vp, i32, vp], ctypes.c_int),
+            "ft8_stft_argmax": ([vp, vp, ctypes.c_int, i64, i32, i64, P, vp, vp], ctypes.c_int),
+            "ft8_drift_fit": ([vp, i32, vp, i32, i32, i32, DP, vp, vp, vp, i32, vp], ctypes.c_int),
+            "ft8_drift_correct": ([vp, vp, ctypes.c_int, i64, i32, i64, DP, vp, vp, vp], ctypes.c_int),
         }
         for name, (args, res) in sig.items():
             fn = getattr(L, name)
@@ -109,7 +135,7 @@ EXPORTED_SYMBOLS = (
     "ft8_create", "ft8_destroy", "ft8_last_error", "ft8_abi_version", "ft8_limits", "ft8_geometry",
     "ft8_stft", "ft8_sync_select", "ft8_llr", "ft8_normalize", "ft8_bp", "ft8_decode_batch", "ft8_select_warnings",
     "ft8_crc14", "ft8_ldpc_check", "ft8_set_timing", "ft8_get_timing", "ft8_get_counters", "ft8_set_pipeline",
-    "ft8_encode", "ft8_synthesize", "ft8_subtract")
+    "ft8_encode", "ft8_synthesize", "ft8_subtract", "ft8_stft_argmax", "ft8_drift_fit", "ft8_drift_correct")
 
 
 def limits():

@@ -53,6 +53,11 @@ struct ft8_ctx {
   // cumulative GFSK pulse of the transmit chain for one nsps (double and float)
   int gfsk_nsps = 0;
   DevBuf gfsk_P, gfsk_Pf;
+  // frequency-drift correction: per-frame argmax, three-Costas correlation template (cached per
+  // steps_per_symbol / nsync / ndata)
+  DevBuf drift_idx, drift_tmpl;
+  int tmpl_key[3] = {0, 0, 0};
+  int tmpl_len = 0;
   bool timing = false;
   std::vector<TimedLaunch> pending;
   std::vector<hipEvent_t> pool;
@@ -632,6 +637,128 @@ int subtract_core(ft8_ctx* c, const void* x, int dtype, float* resid, int64_t n_
   return e == hipSuccess ? FT8_OK : hipfail(c, e, "subtract launch");
 }
 
+// ---- frequency-drift correction ----------------------------------------------------------------
+// kept f >= 0 bins of a two-sided spectrum after fftshift (frequency_correction.py:198-200)
+int drift_bins(int nfft) { return (nfft + 1) / 2; }
+
+int stft_argmax_core(ft8_ctx* c, const void* x, int dtype, int64_t n_samples, int n_slots, int64_t stride,
+                     const ft8_params* p, int32_t* idx, hipStream_t s) {
+  Geo g;
+  std::string why;
+  int rc = geometry(p->sample_rate, p->bins_per_tone, p->steps_per_symbol, n_samples, &g, &why);
+  if (rc) return fail(c, rc, why);
+  if (dtype < FT8_F32 || dtype > FT8_I16) return fail(c, FT8_E_ARG, "unknown sample dtype");
+  if (p->t_lo < 0 || p->t_hi > g.frames || p->t_lo > p->t_hi)
+    return fail(c, FT8_E_ARG, "frame range [t_lo, t_hi) outside [0, " + std::to_string(g.frames) + ")");
+  if (p->f_lo < 0 || p->f_hi > g.nfft || p->f_lo >= p->f_hi) return fail(c, FT8_E_ARG, "bin range [f_lo, f_hi) empty or outside [0, nfft)");
+  if (p->t_hi == p->t_lo || n_slots == 0) return FT8_OK;
+  const bool f64 = is_f64_dtype(dtype), cplx = is_cplx_dtype(dtype);
+  StftLaunch L{};
+  if ((rc = get_plan(c, g.nfft, cplx, f64, &L.plan))) return rc;
+  WinEntry* w = nullptr;
+  if ((rc = get_window(c, g.nperseg, f64, &w))) return rc;
+  L.samples = x;
+  L.dtype = dtype;
+  L.n_samples = n_samples;
+  L.slot_stride = stride;
+  L.n_slots = n_slots;
+  L.nperseg = g.nperseg;
+  L.hop = g.hop;
+  L.nfft = g.nfft;
+  L.t_lo = p->t_lo;
+  L.t_hi = p->t_hi;
+  L.f_lo = p->f_lo;
+  L.f_hi = p->f_hi;
+  L.window = w->w;
+  L.scale = w->scale;
+  L.argmax = idx;
+  StageTimer tm(c, 8, s);
+  hipError_t e = launch_stft(L, s);
+  tm.done();
+  return e == hipSuccess ? FT8_OK : hipfail(c, e, "stft argmax launch");
+}
+
+int check_drift_params(ft8_ctx* c, const ft8_drift_params* p) {
+  if (p->bins_per_tone <= 0 || p->steps_per_symbol <= 0) return fail(c, FT8_E_ARG, "bins_per_tone and steps_per_symbol must be positive");
+  if (p->sample_rate <= 0 || p->sample_rate != std::floor(p->sample_rate) || p->sample_rate > 2e9)
+    return fail(c, FT8_E_UNSUPPORTED, "sample_rate must be a positive integral number of Hz");
+  const int w = p->window_size_factor * p->steps_per_symbol;
+  if (w < 1) return fail(c, FT8_E_ARG, "window_size_factor * steps_per_symbol must be >= 1");
+  if (w > kDriftMaxWindow) return fail(c, FT8_E_RANGE, "continuity window exceeds " + std::to_string(kDriftMaxWindow));
+  if (p->nsync_sym < 1 || p->nsync_sym > 7) return fail(c, FT8_E_ARG, "nsync_sym must be in [1, 7] (the Costas array has 7 tones)");
+  if (p->ndata_sym < 0) return fail(c, FT8_E_ARG, "ndata_sym must be >= 0");
+  if (3 * (p->nsync_sym - 1) * p->steps_per_symbol > drift_max_points())
+    return fail(c, FT8_E_RANGE, "sync regression points exceed the compiled limit");
+  return FT8_OK;
+}
+
+// three_sync_correlation_seq (frequency_correction.py:386-407), NumPy's operation order
+int drift_template(ft8_ctx* c, const ft8_drift_params* p) {
+  const int tosr = p->steps_per_symbol, ns = p->nsync_sym, nd = p->ndata_sym;
+  if (c->tmpl_len > 0 && c->tmpl_key[0] == tosr && c->tmpl_key[1] == ns && c->tmpl_key[2] == nd) return FT8_OK;
+  const int sps2 = 2 * tosr;
+  static const int costas[7] = {3, 1, 4, 0, 6, 5, 2};
+  double seq[7];
+  for (int k = 0; k < 7; ++k) seq[k] = (double)(costas[k] + 1) - 4.0;  // - np.mean(...) = 4.0 exactly
+  // t = np.linspace(-1, 1, sps2 + 1); gfsk_shape = gfsk_pulse(2.0, t)  (:27-40)
+  const double step = 2.0 / (double)sps2;
+  const double kk = M_PI * std::sqrt(2.0 / std::log(2.0));
+  const double kb = kk * 2.0;
+  std::vector<double> shape(sps2 + 1);
+  for (int j = 0; j <= sps2; ++j) {
+    const double t = j == sps2 ? 1.0 : (double)j * step + -1.0;
+    shape[j] = 0.5 * (std::erf(kb * (t + 0.5)) - std::erf(kb * (t - 0.5)));
+  }
+  const int L1 = (ns - 1) * tosr + sps2 + 1;
+  std::vector<double> one(L1, 0.0);
+  for (int k = 0; k < ns; ++k)
+    for (int j = 0; j <= sps2; ++j) one[k * tosr + j] += shape[j] * seq[k];
+  const int L3 = (3 * ns + nd - 1) * tosr + 1 + sps2;
+  if (L3 > drift_max_template()) return fail(c, FT8_E_RANGE, "sync template exceeds the compiled limit");
+  std::vector<double> three(L3, 0.0);
+  for (int i = 0; i < 3; ++i) {
+    const int s0 = i * (ns + nd / 2) * tosr;
+    if (s0 + L1 > L3) return fail(c, FT8_E_ARG, "sync blocks do not fit the template (the reference raises ValueError)");
+    for (int j = 0; j < L1; ++j) three[s0 + j] = one[j];
+  }
+  int rc = ensure(c, c->drift_tmpl, sizeof(double) * L3);
+  if (rc) return rc;
+  hipError_t e = hipMemcpy(c->drift_tmpl.p, three.data(), sizeof(double) * L3, hipMemcpyHostToDevice);
+  if (e != hipSuccess) return hipfail(c, e, "template upload");
+  c->tmpl_key[0] = tosr;
+  c->tmpl_key[1] = ns;
+  c->tmpl_key[2] = nd;
+  c->tmpl_len = L3;
+  return FT8_OK;
+}
+
+int drift_fit_core(ft8_ctx* c, int stage, const int32_t* idx, int n_slots, int T, int F, const ft8_drift_params* p,
+                   ft8_drift_result* res, double* metric, int32_t* segments, int max_segments, hipStream_t s) {
+  int rc = check_drift_params(c, p);
+  if (rc) return rc;
+  if (T > kDriftMaxT) return fail(c, FT8_E_RANGE, "more than " + std::to_string(kDriftMaxT) + " frames per signal");
+  if (F < 1 || F > 8192) return fail(c, FT8_E_RANGE, "freq_bins must be in [1, 8192]");
+  DriftFitLaunch L{};
+  L.idx = idx;
+  L.n_slots = n_slots;
+  L.T = T;
+  L.F = F;
+  L.p = *p;
+  L.res = res;
+  L.metric = metric;
+  L.segments = segments;
+  L.max_segments = segments ? max_segments : 0;
+  if (stage == 2) {
+    if ((rc = drift_template(c, p))) return rc;
+    L.tmpl = (const double*)c->drift_tmpl.p;
+    L.n_tmpl = c->tmpl_len;
+  }
+  StageTimer tm(c, 9, s);
+  hipError_t e = launch_drift_fit(stage, L, s);
+  tm.done();
+  return e == hipSuccess ? FT8_OK : hipfail(c, e, "drift fit launch");
+}
+
 }  // namespace
 
 // ============================================================================================
@@ -666,7 +793,7 @@ int ft8_destroy(ft8_ctx* c) {
     DeviceGuard dg(c->device);
     for (auto* b : {&c->wf, &c->scores, &c->cand, &c->cand_score, &c->cand_count, &c->warn, &c->rowsum,
                     &c->res_all, &c->work, &c->stats, &c->llr, &c->tie, &c->residual, &c->sub_est, &c->out1,
-                    &c->counts1, &c->out2, &c->counts2, &c->gfsk_P, &c->gfsk_Pf})
+                    &c->counts1, &c->out2, &c->counts2, &c->gfsk_P, &c->gfsk_Pf, &c->drift_idx, &c->drift_tmpl})
       if (b->p) (void)hipFree(b->p);
     for (auto& p : c->plans) {
       if (p.tw) (void)hipFree(p.tw);
@@ -903,6 +1030,87 @@ int ft8_subtract(ft8_ctx* c, const void* d_samples, int dtype, float* d_residual
   DeviceGuard dg(c->device);
   return subtract_core(c, d_samples, dtype, d_residual, n_samples, n_slots, slot_stride, slot_stride, p, d_res,
                        d_counts, cap, (hipStream_t)stream);
+}
+
+int ft8_stft_argmax(ft8_ctx* c, const void* d_samples, int dtype, int64_t n_samples, int32_t n_slots,
+                    int64_t slot_stride, const ft8_params* p, int32_t* d_idx, void* stream) {
+  if (!c || !p || (n_slots > 0 && (!d_samples || !d_idx))) return fail(c, FT8_E_ARG, "null argument");
+  if (n_slots < 0 || n_samples < 0) return fail(c, FT8_E_ARG, "negative size");
+  if (n_slots > 1 && slot_stride < n_samples) return fail(c, FT8_E_ARG, "slot_stride < n_samples");
+  DeviceGuard dg(c->device);
+  return stft_argmax_core(c, d_samples, dtype, n_samples, n_slots, slot_stride, p, d_idx, (hipStream_t)stream);
+}
+
+int ft8_drift_fit(ft8_ctx* c, int32_t stage, const int32_t* d_idx, int32_t n_slots, int32_t T, int32_t F,
+                  const ft8_drift_params* p, ft8_drift_result* d_res, double* d_metric, int32_t* d_segments,
+                  int32_t max_segments, void* stream) {
+  if (!c || !p) return fail(c, FT8_E_ARG, "null argument");
+  if (stage != 1 && stage != 2) return fail(c, FT8_E_ARG, "stage must be 1 or 2");
+  if (n_slots < 0 || T < 0 || max_segments < 0) return fail(c, FT8_E_ARG, "negative size");
+  if (n_slots == 0) return FT8_OK;
+  if (!d_res || (T > 0 && !d_idx)) return fail(c, FT8_E_ARG, "null argument");
+  DeviceGuard dg(c->device);
+  return drift_fit_core(c, stage, d_idx, n_slots, T, F, p, d_res, d_metric, d_segments, max_segments,
+                        (hipStream_t)stream);
+}
+
+int ft8_drift_correct(ft8_ctx* c, const void* d_samples, int dtype, int64_t n_samples, int32_t n_slots,
+                      int64_t slot_stride, const ft8_drift_params* p, void* d_out, ft8_drift_result* d_res,
+                      void* stream) {
+  if (!c || !p) return fail(c, FT8_E_ARG, "null argument");
+  if (n_slots < 0 || n_samples < 0) return fail(c, FT8_E_ARG, "negative size");
+  if (n_slots == 0) return FT8_OK;
+  if (!d_samples || !d_out || !d_res) return fail(c, FT8_E_ARG, "null argument");
+  if (n_slots > 1 && slot_stride < n_samples) return fail(c, FT8_E_ARG, "slot_stride < n_samples");
+  if (dtype != FT8_F32 && dtype != FT8_F64 && dtype != FT8_C64 && dtype != FT8_C128)
+    return fail(c, FT8_E_UNSUPPORTED, "drift correction takes float32/float64/complex64/complex128 samples");
+  int rc = check_drift_params(c, p);
+  if (rc) return rc;
+  DeviceGuard dg(c->device);
+  hipStream_t s = (hipStream_t)stream;
+  Geo g;
+  std::string why;
+  const int fs = (int)p->sample_rate;
+  if ((rc = geometry(fs, p->bins_per_tone, p->steps_per_symbol, n_samples, &g, &why))) return fail(c, rc, why);
+  if (g.frames == 0) return fail(c, FT8_E_ARG, "input shorter than one symbol (the reference's argmax of an empty spectrogram raises)");
+  if (g.frames > kDriftMaxT) return fail(c, FT8_E_RANGE, "more than " + std::to_string(kDriftMaxT) + " frames per signal");
+  const int T = g.frames, F = drift_bins(g.nfft);
+  if ((rc = ensure(c, c->drift_idx, sizeof(int32_t) * (size_t)n_slots * T))) return rc;
+  int32_t* idx = (int32_t*)c->drift_idx.p;
+  ft8_params sp{};
+  sp.sample_rate = fs;
+  sp.bins_per_tone = p->bins_per_tone;
+  sp.steps_per_symbol = p->steps_per_symbol;
+  sp.f_lo = 0;
+  sp.f_hi = F;
+  sp.t_lo = 0;
+  sp.t_hi = T;
+  if ((rc = stft_argmax_core(c, d_samples, dtype, n_samples, n_slots, slot_stride, &sp, idx, s))) return rc;
+  if ((rc = drift_fit_core(c, 1, idx, n_slots, T, F, p, d_res, nullptr, nullptr, 0, s))) return rc;
+  DerotateLaunch D{};
+  D.x = d_samples;
+  D.dtype = dtype;
+  D.slot_stride = slot_stride;
+  D.out = (double*)d_out;
+  D.n_samples = n_samples;
+  D.n_slots = n_slots;
+  D.res = d_res;
+  D.fs = p->sample_rate;
+  D.inv_fs = 1.0 / p->sample_rate;
+  D.inv_2fs2 = 1.0 / (2.0 * p->sample_rate * p->sample_rate);
+  {
+    StageTimer tm(c, 10, s);
+    hipError_t e = launch_derotate1(D, s);
+    tm.done();
+    if (e != hipSuccess) return hipfail(c, e, "derotate launch");
+  }
+  if (!p->precise_sync) return FT8_OK;
+  if ((rc = stft_argmax_core(c, d_out, FT8_C128, n_samples, n_slots, n_samples, &sp, idx, s))) return rc;
+  if ((rc = drift_fit_core(c, 2, idx, n_slots, T, F, p, d_res, nullptr, nullptr, 0, s))) return rc;
+  StageTimer tm(c, 10, s);
+  hipError_t e = launch_derotate2(D, p->poly_degree, s);
+  tm.done();
+  return e == hipSuccess ? FT8_OK : hipfail(c, e, "derotate launch");
 }
 
 int ft8_set_pipeline(ft8_ctx* c, int32_t chunk_slots, int32_t n_streams, int32_t bp_waves_per_simd) {

@@ -44,6 +44,7 @@ struct StftLaunch {
   const void* window;      // float or double [nperseg]
   double scale;            // 1 / (sum w)^2
   void* out;               // float or double [n_slots][t_hi-t_lo][f_hi-f_lo]
+  int32_t* argmax;         // non-null: write per-frame argmax over the kept bins instead of `out`
   FftPlan plan;
 };
 hipError_t launch_stft(const StftLaunch& a, hipStream_t s);
@@ -189,6 +190,39 @@ hipError_t launch_subtract(const SubLaunch& a, hipStream_t s);
 hipError_t launch_merge_pass(ft8_result* out, int32_t* counts, int cap, const ft8_result* out1,
                              const int32_t* counts1, int cap1, const ft8_result* out2, const int32_t* counts2,
                              int cap2, int n_slots, hipStream_t s);
+
+// ---- frequency-drift correction (drift.hip) ---------------------------------------------------
+struct DriftFitLaunch {
+  const int32_t* idx;          // [n_slots][T] per-frame argmax (kept-bin index)
+  int n_slots, T, F;
+  ft8_drift_params p;
+  ft8_drift_result* res;       // [n_slots]
+  double* metric;              // [n_slots][T - window + 1] or null
+  int32_t* segments;           // [n_slots][max_segments][2] or null
+  int max_segments;
+  const double* tmpl;          // stage 2: three_sync_correlation_seq [n_tmpl]
+  int n_tmpl;
+};
+constexpr int kDriftMaxT = 16384;   // frames per signal held in LDS by the fit kernels
+hipError_t launch_drift_fit(int stage, const DriftFitLaunch& a, hipStream_t s);
+
+struct DerotateLaunch {
+  const void* x;               // stage 1: input samples (dtype), row stride slot_stride
+  int dtype;
+  int64_t slot_stride;
+  double* out;                 // complex128 [n_slots][n_samples] (interleaved re, im)
+  int64_t n_samples;
+  int n_slots;
+  const ft8_drift_result* res;
+  double fs, inv_fs, inv_2fs2; // fs, fl(1/fs), fl(1/(2 fs^2)) (NumPy divides complex by real via 1/d)
+};
+// stage 1: out = x * exp(-2 pi i rate1 n^2 / (2 fs^2))  (x itself for FT8_DRIFT_NO_SEGMENT)
+hipError_t launch_derotate1(const DerotateLaunch& a, hipStream_t s);
+// stage 2: out *= the polynomial carrier of degree deg (1 or 2) where the status is FT8_DRIFT_FULL
+hipError_t launch_derotate2(const DerotateLaunch& a, int deg, hipStream_t s);
+int drift_max_template();      // LDS capacity of k_drift_fit2: template length, regression points
+int drift_max_points();
+constexpr int kDriftMaxWindow = 64;  // continuity window (exact int64 sums)
 
 hipError_t launch_crc14(const uint8_t* msg, const int32_t* nbits, int n, uint16_t* crc, hipStream_t s);
 hipError_t launch_ldpc_check(const uint8_t* bits, int n, int32_t* err, hipStream_t s);

@@ -241,14 +241,32 @@ struct StftArgs {
   int radix[16];
   const void* tw;
   const void* post;
+  int32_t* argmax;  // non-null: per-frame argmax of the kept dB row instead of the row itself
+  int n_slots, per_xcd;
 };
+
+// np.argmax order: the first NaN wins, else the largest value, ties to the lower index
+template <typename CT>
+__device__ __forceinline__ bool argmax_better(CT av, int ai, CT bv, int bi) {
+  const bool an = av != av, bn = bv != bv;
+  if (an != bn) return an;
+  if (!an && av != bv) return av > bv;
+  return ai < bi;
+}
 
 template <typename InT, bool CPLX, typename CT, int MAXV>
 __global__ __launch_bounds__(kThreads) void k_stft(StftArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   cplx<CT>* buf = reinterpret_cast<cplx<CT>*>(smem);
-  const int frame = a.t_lo + blockIdx.x;
-  const int slot = blockIdx.y;
+  // XCD-aware order: hardware deals workgroup ids round-robin over the 8 XCDs, so consecutive
+  // ids would put neighbouring (overlapping) frames on different L2s.  Each XCD instead takes a
+  // contiguous run of (slot, frame) pairs, and overlapping frames share its L2.
+  const int nt = a.nt_out;
+  const int r = (int)(blockIdx.x & 7) * a.per_xcd + (int)(blockIdx.x >> 3);
+  if (r >= nt * a.n_slots) return;
+  const int slot = r / nt;
+  const int fi = r - slot * nt;
+  const int frame = a.t_lo + fi;
   const InT* xs = reinterpret_cast<const InT*>(a.samples) +
                   (int64_t)slot * a.slot_stride * (CPLX ? 2 : 1) + (int64_t)frame * a.hop * (CPLX ? 2 : 1);
   FrameSrc<InT, CPLX, CT> src{xs, reinterpret_cast<const CT*>(a.window), a.nperseg};
@@ -265,9 +283,12 @@ __global__ __launch_bounds__(kThreads) void k_stft(StftArgs a) {
 
   // epilogue: power spectrum -> dB for bins [f_lo, f_lo + nf_out)
   const CT scale = (CT)a.scale;
-  CT* out = reinterpret_cast<CT*>(a.out) + ((int64_t)slot * a.nt_out + blockIdx.x) * a.nf_out;
+  const bool amax = a.argmax != nullptr;
+  CT* out = reinterpret_cast<CT*>(a.out) + ((int64_t)slot * a.nt_out + fi) * a.nf_out;
   const int N = a.nfft;
   const cplx<CT>* post = reinterpret_cast<const cplx<CT>*>(a.post);
+  CT bv = -__builtin_huge_val();
+  int bi = 0x7fffffff;
   for (int i = threadIdx.x; i < a.nf_out; i += kThreads) {
     const int k = a.f_lo + i;
     cplx<CT> X;
@@ -284,12 +305,37 @@ __global__ __launch_bounds__(kThreads) void k_stft(StftArgs a) {
       X = {(CT)0.5 * (s.x + wd.y), (CT)0.5 * (s.y - wd.x)};
     }
     const CT pw = (X.x * X.x + X.y * X.y) * scale;
+    CT db;
     if constexpr (sizeof(CT) == 4) {
       const float v = 1e-12f + pw;
-      out[i] = 10.0f * log10f(v);
+      db = 10.0f * log10f(v);
     } else {
-      out[i] = 10.0 * log10(1e-12 + pw);
+      db = 10.0 * log10(1e-12 + pw);
     }
+    if (amax) {
+      if (argmax_better(db, i, bv, bi)) { bv = db; bi = i; }
+    } else {
+      out[i] = db;
+    }
+  }
+  if (!amax) return;
+  // workgroup argmax: within each wave by shuffles, then across the waves through LDS
+#pragma unroll
+  for (int off = kWave / 2; off > 0; off >>= 1) {
+    const CT ov = __shfl_xor(bv, off);
+    const int oi = __shfl_xor(bi, off);
+    if (argmax_better(ov, oi, bv, bi)) { bv = ov; bi = oi; }
+  }
+  __syncthreads();  // every thread is done reading the spectrum in buf
+  CT* sv = reinterpret_cast<CT*>(smem);
+  int* si = reinterpret_cast<int*>(smem + sizeof(CT) * (kThreads / kWave));
+  const int w = threadIdx.x / kWave;
+  if ((threadIdx.x & (kWave - 1)) == 0) { sv[w] = bv; si[w] = bi; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int k = 1; k < kThreads / kWave; ++k)
+      if (argmax_better(sv[k], si[k], bv, bi)) { bv = sv[k]; bi = si[k]; }
+    a.argmax[(int64_t)slot * nt + fi] = bi;
   }
 }
 
@@ -529,7 +575,7 @@ __global__ __launch_bounds__(k38Threads) void k_stft3840(StftArgs a) {
 
 template <typename InT, bool CPLX, typename CT>
 hipError_t launch_t(const StftLaunch& L, const StftArgs& a, hipStream_t s) {
-  dim3 grid(L.t_hi - L.t_lo, L.n_slots);
+  const dim3 grid((unsigned)(8 * a.per_xcd));  // see k_stft: a.per_xcd (slot, frame) pairs per XCD
   const size_t lds = (size_t)a.P * sizeof(cplx<CT>);
   auto go = [&](auto kern) {
     if (lds > 64 * 1024) {
@@ -566,9 +612,12 @@ hipError_t launch_stft(const StftLaunch& L, hipStream_t s) {
   for (int i = 0; i < 16; ++i) a.radix[i] = L.plan.radix[i];
   a.tw = L.plan.tw;
   a.post = L.plan.post;
+  a.argmax = L.argmax;
+  a.n_slots = L.n_slots;
+  a.per_xcd = (int)(((int64_t)a.nt_out * L.n_slots + 7) / 8);
   if (a.nt_out <= 0 || a.nf_out <= 0 || L.n_slots <= 0) return hipSuccess;
   // production geometry: 12 kHz, bins_per_tone = steps_per_symbol = 2 (pairs need an even stride)
-  if ((L.dtype == FT8_F32 || L.dtype == FT8_I16) && L.nfft == 2 * k38P && L.nperseg == k38P && L.hop == 960 &&
+  if (!L.argmax && (L.dtype == FT8_F32 || L.dtype == FT8_I16) && L.nfft == 2 * k38P && L.nperseg == k38P && L.hop == 960 &&
       a.P == k38P && (L.slot_stride % 2) == 0) {
     const int chunks = (a.nt_out + k38Chunk - 1) / k38Chunk;
     const dim3 grid((unsigned)(chunks * L.n_slots));

@@ -226,9 +226,79 @@ int ft8_subtract(ft8_ctx* ctx, const void* d_samples, int dtype, float* d_residu
                  int32_t n_slots, int64_t slot_stride, const ft8_params* p, const ft8_result* d_res,
                  const int32_t* d_counts, int32_t cap, void* stream);
 
+/* ---- frequency-drift correction (ft8_beacon_receiver/frequency_correction.py) -------------
+ * Paths below are relative to src/ft8_tools/ft8_beacon_receiver/.  Parameters of
+ * correct_frequency_drift (frequency_correction.py:118-163); fields default to the reference's
+ * default_params when the Python mirror fills them. */
+typedef struct ft8_drift_params {
+  double sample_rate;          /* fs, Hz (integral) */
+  double sym_bin;              /* symbol frequency spacing, Hz (6.25) */
+  double sym_t;                /* symbol time, s (0.16) */
+  double max_variance_factor;  /* max_variance = factor * freq_bins^2 */
+  int32_t bins_per_tone;       /* freq_osr */
+  int32_t steps_per_symbol;    /* time_osr */
+  int32_t nsync_sym, ndata_sym;
+  int32_t window_size_factor;  /* window_size = factor * steps_per_symbol */
+  int32_t fit_middle_percent;
+  int32_t poly_degree;
+  int32_t precise_sync;
+} ft8_drift_params;
+
+/* how correct_frequency_drift returned (frequency_correction.py line of the return) */
+enum ft8_drift_status {
+  FT8_DRIFT_PENDING = 0,       /* stage 1 done, stage 2 not yet run */
+  FT8_DRIFT_NO_SEGMENT = 1,    /* :236  no continuous segment: the input is returned, rate 0 */
+  FT8_DRIFT_LINEAR = 2,        /* :359  precise_sync off: linear compensation only */
+  FT8_DRIFT_FEW_POINTS = 3,    /* :523  < 10 sync regression points: linear compensation */
+  FT8_DRIFT_DEGREE = 4,        /* :631  poly_degree not 1 or 2: linear compensation */
+  FT8_DRIFT_FULL = 5,          /* :655  linear + polynomial compensation */
+  FT8_DRIFT_UNDERDETERMINED = 6, /* :659 points <= poly_degree + 1: linear compensation */
+  FT8_DRIFT_VALUE_ERROR = -1  /* the reference raises ValueError inside LinearRegression.fit
+                                 (:337 an empty segment, :539 regression x/y lengths differ) */
+};
+
+/* Per-slot outcome, 72 bytes. */
+typedef struct ft8_drift_result {
+  double rate_per_sample;      /* correct_frequency_drift's second return value */
+  double rate1;                /* f_shift_rate of the linear pass, Hz/s (:348) */
+  double coef[3];              /* coefs_final[0..2] of the polynomial fit (coef[0] = 0) */
+  double intercept;            /* intercept_final */
+  int32_t status;              /* ft8_drift_status */
+  int32_t n_segments;          /* continuity segments found (detect_signal_continuity) */
+  int32_t seg_start, seg_end;  /* longest segment (max by end - start, first on ties) */
+  int32_t sync_idx;            /* correlation_peak_time_block_index (:463) */
+  int32_t n_points;            /* regression points of the polynomial fit */
+} ft8_drift_result;
+
+/* calculate_spectrogram -> kept bins -> np.argmax over frequency per frame, without writing the
+ * waterfall (the argmax is fused into the STFT epilogue): d_idx[n_slots][t_hi - t_lo] = the first
+ * bin index (relative to f_lo) of the largest dB value of each frame (frequency_correction.py:
+ * 190-224, 364-384).  Samples and params as for ft8_stft. */
+int ft8_stft_argmax(ft8_ctx* ctx, const void* d_samples, int dtype, int64_t n_samples, int32_t n_slots,
+                    int64_t slot_stride, const ft8_params* p, int32_t* d_idx, void* stream);
+
+/* The two estimation stages on per-frame argmax indices d_idx[n_slots][T] (F = kept bins):
+ * stage 1: detect_signal_continuity (:42-115) + longest segment + linear fit (:227-348) -> d_res
+ *          (d_metric[n_slots][T - window + 1], nullable: the continuity metric; d_segments
+ *          [n_slots][max_segments][2], nullable: the first max_segments segments);
+ * stage 2: d_idx of the linearly compensated signal -> sync correlation (:386-463) + polynomial
+ *          fit (:502-590) -> d_res (which must hold the stage-1 result). */
+int ft8_drift_fit(ft8_ctx* ctx, int32_t stage, const int32_t* d_idx, int32_t n_slots, int32_t T, int32_t F,
+                  const ft8_drift_params* p, ft8_drift_result* d_res, double* d_metric, int32_t* d_segments,
+                  int32_t max_segments, void* stream);
+
+/* Replaces correct_frequency_drift (frequency_correction.py:118-659) for a batch of independent
+ * signals: STFT-argmax -> stage 1 -> linear de-rotation -> STFT-argmax -> stage 2 -> polynomial
+ * de-rotation, all on the device.  d_samples: dtype F32/F64/C64/C128, row stride slot_stride
+ * elements.  d_out: complex128 [n_slots][n_samples] (for FT8_DRIFT_NO_SEGMENT the input converted
+ * to complex128).  d_res[n_slots].  De-rotation carriers: :352 and :598-611. */
+int ft8_drift_correct(ft8_ctx* ctx, const void* d_samples, int dtype, int64_t n_samples, int32_t n_slots,
+                      int64_t slot_stride, const ft8_drift_params* p, void* d_out, ft8_drift_result* d_res,
+                      void* stream);
+
 /* ---- per-stage device timing (HIP events on the caller's stream) --------------------------- */
-#define FT8_N_STAGES 8 /* 0 stft, 1 score, 2 select, 3 bp, 4 compact, 5 whole decode_batch, 6 llr,
-                        7 subtract */
+#define FT8_N_STAGES 11 /* 0 stft, 1 score, 2 select, 3 bp, 4 compact, 5 whole decode_batch, 6 llr,
+                         7 subtract, 8 drift STFT-argmax, 9 drift fits, 10 drift de-rotation */
 int ft8_set_timing(ft8_ctx* ctx, int enable);
 /* accumulated milliseconds and launch counts per stage since the last reset; synchronises. */
 int ft8_get_timing(ft8_ctx* ctx, double* ms, int64_t* launches, int reset);

@@ -38,3 +38,19 @@ def gpu():
         pytest.skip("no GPU")
     torch.cuda.set_device(0)
     return torch
+
+
+@pytest.fixture(scope="session")
+def drift_golden():
+    with open(os.path.join(GOLD, "drift.json")) as f:
+        meta = json.load(f)
+    return meta, np.load(os.path.join(GOLD, "drift.npz"), allow_pickle=False)
+
+
+@pytest.fixture(scope="session")
+def drift_inputs(drift_golden, oracle):
+    """Golden-case inputs regenerated from their parameters (oracle/drift.py beacon_input)."""
+    from oracle import drift as OD
+    meta, _ = drift_golden
+    return {c["name"]: OD.beacon_input(c["payload"], c["fs"], c["f0"], c["fc"], c["drift_hz_per_s"],
+                                       c["esn0_db"], c["seed"]) for c in meta["cases"]}
