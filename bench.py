@@ -16,6 +16,9 @@ Prints ONE JSON line on rank 0.  Besides the contract fields it carries:
   bp_stress     BASELINE config 4 first pass: 100k LLR vectors x 50 BP iterations, candidates/s (N=1)
   subtract_redecode  BASELINE config 4 with the subtract-and-redecode second pass: 334 crowded
                 slots x K=300 (top-k), 50 iterations, both passes, candidates/s (N=1)
+  drift_correct the beacon receiver's frequency-drift correction on a batch of 256
+                complex128 beacon signals (12 kHz, 3 x 12.64 s, steps_per_symbol 8): signals/s, the
+                dominant kernel's roofline and the oracle port's CPU rate (N=1)
   h2d_stream    the same slots as int16 PCM in pinned host memory, upload overlapped with decode (N=1)
   cpu_baseline  the oracle port (oracle/, C + scipy) on a bounded sample of the same slots (rank 0, N=1)
 """
@@ -165,6 +168,121 @@ def subtract_redecode(dev, n_slots=334, signals=50, iters=50, reps=3):
                     "has no second pass"}
 
 
+DRIFT_PARAMS = {"bins_per_tone": 2, "steps_per_symbol": 8}  # the reference test's correction params
+
+
+def drift_worker(args):
+    from oracle import drift as OD
+    hexp, f0, fc, drift, seed = args
+    x = OD.beacon_input(hexp, 12000, f0, fc, drift, 28.0, seed)
+    t0 = time.perf_counter()
+    OD.correct_frequency_drift(x, 12000, 6.25, 0.16, params=dict(DRIFT_PARAMS))
+    return time.perf_counter() - t0
+
+
+def drift_signal_params(n, seed=4242):
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    return [(bytes(rng.integers(0, 256, 10, dtype=np.uint8)).hex(), float(rng.uniform(200, 500)),
+             float(rng.uniform(300, 700)), float(rng.uniform(50, 150)), int(seed + i)) for i in range(n)]
+
+
+def drift_cpu_baseline(procs, n=32):
+    """oracle/drift.py (NumPy/SciPy restatement of correct_frequency_drift) on n signals of the
+    drift workload, `procs` processes; each worker times only the correction (not the synthesis)."""
+    import multiprocessing as mp
+    ctx = mp.get_context("fork")
+    work = drift_signal_params(n)
+    with ctx.Pool(procs) as pool:
+        pool.map(drift_worker, work[:procs])  # warm imports / FFT plans
+        t0 = time.perf_counter()
+        per = pool.map(drift_worker, work, chunksize=1)
+        dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "signals/s", "cores": procs, "kind": "port",
+            "sample": f"{n} beacon signals of the drift workload, oracle/drift.py (NumPy + scipy "
+                      f"spectrogram), {procs} processes, {dt:.2f} s wall, {sum(per) / n:.2f} s per signal",
+            "wall_s": dt}
+
+
+def drift_correct(dev, n_sig=256, reps=5):
+    """The beacon receiver's correct_frequency_drift (frequency_correction.py:118-659) on a batch of
+    n_sig independent complex128 beacons: 12 kHz, the reference test's layout (12.64 s of signal
+    between two 12.64 s zero-signal pads, 455 040 samples), drift U(50, 150) Hz/s, Es/N0 28 dB,
+    bins_per_tone 2, steps_per_symbol 8, poly_degree 2, precise sync.  Inputs resident in HBM."""
+    import ctypes
+    import numpy as np
+    import torch
+    from ft8_demodulator_amd import _lib, ft8_generator as G
+    from ft8_demodulator_amd.frequency_correction import _drift_params, DEFAULT_PARAMS
+    fs, nsps = 12000, 1920
+    L = 79 * nsps
+    n = 3 * L
+    prm = drift_signal_params(n_sig)
+    pays = np.frombuffer(b"".join(bytes.fromhex(p[0]) for p in prm), dtype=np.uint8).reshape(-1, 10)
+    _, _, tones = G.encode_batch(pays, device=dev)
+    sig = np.array([(p[1] + p[2], 1.0, 0.0, L, i, 0) for i, p in enumerate(prm)], dtype=_lib.TX_SIGNAL_DTYPE)
+    x = G.synthesize(tones, sig, n_sig, n, fs, _lib.FT8_TX_REFERENCE, dtype=torch.complex128, device=dev)
+    t = torch.arange(n, device=dev, dtype=torch.float64)
+    k = torch.tensor([p[3] for p in prm], device=dev, dtype=torch.float64)[:, None] / fs
+    x *= torch.polar(torch.ones((), device=dev, dtype=torch.float64), 2 * np.pi * k * t * t / (2 * fs))
+    es = (x.abs() ** 2).mean(dim=1, keepdim=True)
+    sd = torch.sqrt(es / 10 ** 2.8 * fs / 2)
+    g = torch.Generator(device=dev)
+    g.manual_seed(7)
+    x += torch.complex(torch.randn(x.shape, generator=g, device=dev, dtype=torch.float64),
+                       torch.randn(x.shape, generator=g, device=dev, dtype=torch.float64)) * sd
+    del t
+    ctx = _lib.context(dev)
+    out = torch.empty_like(x)
+    res = torch.zeros(n_sig * _lib.DRIFT_RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+    p = _drift_params(dict(DEFAULT_PARAMS, **DRIFT_PARAMS), fs, 6.25, 0.16)
+    st = _lib.stream_handle(dev)
+
+    def run():
+        ctx.check(_lib.lib().ft8_drift_correct(ctx.handle, _lib.ptr(x), _lib.FT8_C128, n, n_sig, n, ctypes.byref(p),
+                                               _lib.ptr(out), _lib.ptr(res), st), "ft8_drift_correct")
+
+    run()
+    torch.cuda.synchronize()
+    r = res.cpu().numpy().view(_lib.DRIFT_RESULT_DTYPE)
+    est = np.asarray(r["rate_per_sample"]) * fs
+    true = np.array([p_[3] for p_ in prm])
+    ok = r["status"] == _lib.FT8_DRIFT_FULL
+    ctx.set_timing(True)
+    ctx.timing(reset=True)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        run()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    ctx.set_timing(False)
+    tm = ctx.timing(reset=True)
+    stages = {k_: v[0] / reps for k_, v in tm.items() if v[1] > 0 and k_.startswith("drift")}
+    _, hop, nfft, T = _lib.geometry(fs, 2, 8, n)
+    # algorithmic work of one STFT-argmax launch: a 3840-point complex float64 FFT per frame
+    # (5 N log2 N flops) + window (6 N) + |X|^2 of the kept half (3 N/2); 2 launches per call
+    fft_flops = n_sig * T * (5 * nfft * np.log2(nfft) + 6 * nfft + 1.5 * nfft)
+    stft_ms = tm["drift_stft_argmax"][0] / max(tm["drift_stft_argmax"][1], 1)
+    tf = fft_flops / (stft_ms * 1e-3) / 1e12
+    # de-rotation: stage 1 reads 16 B and writes 16 B per sample, stage 2 reads and writes 16 B
+    rot_bytes = n_sig * n * 64
+    rot_ms = tm["drift_derotate"][0] / reps
+    del x, out
+    return {"workload": f"correct_frequency_drift on {n_sig} complex128 beacons x {n} samples (12 kHz, "
+                        "signal between two zero-signal pads as in test_correction.py), drift U(50,150) Hz/s, "
+                        "Es/N0 28 dB, bins_per_tone 2, steps_per_symbol 8, poly_degree 2, precise_sync",
+            "signals_per_s": n_sig * reps / dt, "ms_per_launch": dt / reps * 1e3,
+            "full_fits": int(ok.sum()), "median_abs_rate_err_hz_per_s": float(np.median(np.abs(est[ok] - true[ok]))),
+            "stages_ms": stages,
+            "roofline": {"kernel": "k_stft (argmax epilogue, complex128)", "bound": "fp64-valu", "achieved": tf,
+                         "peak": FP64_VECTOR_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": tf / FP64_VECTOR_PEAK_TFLOPS,
+                         "flops_per_launch": fft_flops, "launch_ms": stft_ms},
+            "roofline_derotate": {"kernel": "k_derotate1 + k_derotate2", "bound": "hbm",
+                                  "achieved": rot_bytes / (rot_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                  "frac": rot_bytes / (rot_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "bytes_per_call": rot_bytes},
+            "data": "synthetic (HIP transmit chain, reference GFSK timing; seeded drift and noise)"}
+
+
 def h2d_stream(x, steps, kw):
     """Slots handed over as 16-bit PCM in pinned host memory (the WAV ingestion path): the upload of
     batch k+1 on a copy stream overlaps the decode of batch k.  PCIe-inclusive slots/s -- reported
@@ -201,6 +319,7 @@ def main():
     ap.add_argument("--no-bp-stress", action="store_true", help="skip the config-4 BP stress leg")
     ap.add_argument("--no-h2d", action="store_true", help="skip the PCIe-inclusive streaming leg")
     ap.add_argument("--no-subtract", action="store_true", help="skip the config-4 subtract-and-redecode leg")
+    ap.add_argument("--no-drift", action="store_true", help="skip the frequency-drift correction leg")
     args = ap.parse_args()
 
     import torch
@@ -210,10 +329,12 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     kw = dict(max_candidates=300, min_score=2, max_iterations=20)
-    cpu = None
+    cpu = drift_cpu_port = None
     if rank == 0 and world == 1 and not args.no_cpu and args.cpu_slots > 0:
         procs = max(1, min(16, len(os.sched_getaffinity(0))))
         cpu = cpu_baseline(kw, min(args.cpu_slots, args.slots), procs, 100000, args.signals)
+        if not args.no_drift:
+            drift_cpu_port = drift_cpu_baseline(procs)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
@@ -289,6 +410,10 @@ def main():
     stream = None
     if world == 1 and not args.no_h2d:
         stream = h2d_stream(x, max(3, min(args.steps, 10)), kw)
+    drift = None
+    if world == 1 and not args.no_drift:
+        drift = drift_correct(dev)
+        drift["cpu_baseline"] = drift_cpu_port
     sub = None
     if world == 1 and not args.no_subtract:
         sub = subtract_redecode(dev)
@@ -339,6 +464,7 @@ def main():
         "bp_stress": stress,
         "h2d_stream": stream,
         "subtract_redecode": sub,
+        "drift_correct": drift,
         "cpu_baseline": cpu,
     }
     if rank == 0:

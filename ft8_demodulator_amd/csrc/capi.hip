@@ -239,9 +239,12 @@ bool factor(int P, FftPlan& pl) {
       r /= f;
     }
   };
+  // few, large register-resident stages: every stage is one LDS round trip
+  take(16);
   take(8);
   take(4);
   take(2);
+  take(15);
   take(5);
   take(3);
   take(7);

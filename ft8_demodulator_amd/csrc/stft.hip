@@ -9,7 +9,8 @@
 // trick: z[n] = w x[2n] + i w x[2n+1] is transformed with a P = nfft/2 point complex FFT and the
 // spectrum of the real frame is recovered as X[k] = (Z[k] + Z*[P-k])/2 - i W_N^k (Z[k] - Z*[P-k])/2,
 // halving the FFT work.  Complex (I/Q) input transforms the full nfft points.  The FFT is a
-// Stockham autosort mixed-radix (2,3,4,5,7,8) transform held in LDS: every stage loads its
+// Stockham autosort mixed-radix (16,8,4,2,15,5,3,7; largest first, so a 3840-point
+// transform is 16 x 16 x 15: three LDS round trips) transform held in LDS: every stage loads its
 // butterflies into registers, barriers, and writes the permuted outputs back, so one LDS buffer of
 // P complex values suffices (15 KB fp32 at 12 kHz).  The first stage reads the frame straight from
 // HBM (coalesced across lanes, window applied on the fly), the epilogue writes the kept bins of the
@@ -142,6 +143,56 @@ struct Dft<7, T> {
   }
 };
 
+// 16 = 4 x 4 (Cooley-Tukey, internal twiddles W_16^(n2 k1)), output in natural order
+template <typename T>
+struct Dft<16, T> {
+  __device__ static void run(cplx<T>* a) {
+    const T c1 = (T)0.92387953251128675613, s1 = (T)0.38268343236508977173, r = (T)0.70710678118654752440;
+    cplx<T> A[4][4];  // [n2][k1]
+#pragma unroll
+    for (int n2 = 0; n2 < 4; ++n2) {
+      cplx<T> v[4] = {a[n2], a[4 + n2], a[8 + n2], a[12 + n2]};
+      Dft<4, T>::run(v);
+#pragma unroll
+      for (int k1 = 0; k1 < 4; ++k1) A[n2][k1] = v[k1];
+    }
+    // W_16^m = exp(-2 pi i m / 16), m = n2 k1 in [0, 9]
+    const cplx<T> w[10] = {{(T)1, (T)0}, {c1, -s1}, {r, -r}, {s1, -c1}, {(T)0, (T)-1},
+                           {-s1, -c1}, {-r, -r}, {-c1, -s1}, {(T)-1, (T)0}, {-c1, s1}};
+#pragma unroll
+    for (int n2 = 1; n2 < 4; ++n2)
+#pragma unroll
+      for (int k1 = 1; k1 < 4; ++k1) A[n2][k1] = cmul(A[n2][k1], w[n2 * k1]);
+#pragma unroll
+    for (int k1 = 0; k1 < 4; ++k1) {
+      cplx<T> v[4] = {A[0][k1], A[1][k1], A[2][k1], A[3][k1]};
+      Dft<4, T>::run(v);
+#pragma unroll
+      for (int k2 = 0; k2 < 4; ++k2) a[k1 + 4 * k2] = v[k2];
+    }
+  }
+};
+// 15 = 3 x 5 prime-factor (no internal twiddles): n = (5 n1 + 3 n2) mod 15, k = (10 k1 + 6 k2) mod 15
+template <typename T>
+struct Dft<15, T> {
+  __device__ static void run(cplx<T>* a) {
+    cplx<T> Y[3][5];
+#pragma unroll
+    for (int n1 = 0; n1 < 3; ++n1) {
+#pragma unroll
+      for (int n2 = 0; n2 < 5; ++n2) Y[n1][n2] = a[(5 * n1 + 3 * n2) % 15];
+      Dft<5, T>::run(Y[n1]);
+    }
+#pragma unroll
+    for (int k2 = 0; k2 < 5; ++k2) {
+      cplx<T> v[3] = {Y[0][k2], Y[1][k2], Y[2][k2]};
+      Dft<3, T>::run(v);
+#pragma unroll
+      for (int k1 = 0; k1 < 3; ++k1) a[(10 * k1 + 6 * k2) % 15] = v[k1];
+    }
+  }
+};
+
 // ---- frame loader: FFT input z[idx] of frame `frame` of slot `slot` --------------------------
 template <typename InT>
 __device__ __forceinline__ float load_f32(const InT* p, int64_t i);
@@ -178,6 +229,11 @@ struct FrameSrc {
   }
 };
 
+// LDS index with one pad element per 16: the Stockham writes of the early stages go out with a
+// stride of R complex values across lanes (16 x 16 B = 256 B for float64 radix 16, every lane on the
+// same banks); padded, the stride is 17 and a 64-lane write needs the minimum number of passes.
+__device__ __forceinline__ int pidx(int i) { return i + (i >> 4); }
+
 // One Stockham stage of radix R.  MAXV = max complex values per thread (P <= 256 * MAXV).
 template <int R, int MAXV, bool FIRST, typename CT, typename Src>
 __device__ __forceinline__ void stockham_stage(cplx<CT>* buf, int P, int Ns, const cplx<CT>* tw,
@@ -193,7 +249,7 @@ __device__ __forceinline__ void stockham_stage(cplx<CT>* buf, int P, int Ns, con
 #pragma unroll
       for (int r = 0; r < R; ++r) {
         if constexpr (FIRST) v[b][r] = src(j + r * nbf);
-        else v[b][r] = buf[j + r * nbf];
+        else v[b][r] = buf[pidx(j + r * nbf)];
       }
     }
   }
@@ -211,7 +267,7 @@ __device__ __forceinline__ void stockham_stage(cplx<CT>* buf, int P, int Ns, con
       Dft<R, CT>::run(v[b]);
       const int d0 = (j / Ns) * Ns * R + k;
 #pragma unroll
-      for (int r = 0; r < R; ++r) buf[d0 + r * Ns] = v[b][r];
+      for (int r = 0; r < R; ++r) buf[pidx(d0 + r * Ns)] = v[b][r];
     }
   }
   __syncthreads();
@@ -225,6 +281,8 @@ __device__ void run_stage(int R, cplx<CT>* buf, int P, int Ns, const cplx<CT>* t
     case 4: stockham_stage<4, MAXV, FIRST>(buf, P, Ns, tw, src); break;
     case 5: stockham_stage<5, MAXV, FIRST>(buf, P, Ns, tw, src); break;
     case 7: stockham_stage<7, MAXV, FIRST>(buf, P, Ns, tw, src); break;
+    case 15: stockham_stage<15, MAXV, FIRST>(buf, P, Ns, tw, src); break;
+    case 16: stockham_stage<16, MAXV, FIRST>(buf, P, Ns, tw, src); break;
     default: stockham_stage<8, MAXV, FIRST>(buf, P, Ns, tw, src); break;
   }
 }
@@ -255,7 +313,9 @@ __device__ __forceinline__ bool argmax_better(CT av, int ai, CT bv, int bi) {
 }
 
 template <typename InT, bool CPLX, typename CT, int MAXV>
-__global__ __launch_bounds__(kThreads) void k_stft(StftArgs a) {
+// two resident waves per SIMD for P <= 4096 (the LDS allows two float64 3840-point workgroups per
+// CU; the radix-16/15 stages then fit 256 VGPRs), one for the 8192-point variant
+__global__ __launch_bounds__(kThreads, (MAXV <= 16 ? 2 : 1)) void k_stft(StftArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   cplx<CT>* buf = reinterpret_cast<cplx<CT>*>(smem);
   // XCD-aware order: hardware deals workgroup ids round-robin over the 8 XCDs, so consecutive
@@ -283,21 +343,18 @@ __global__ __launch_bounds__(kThreads) void k_stft(StftArgs a) {
 
   // epilogue: power spectrum -> dB for bins [f_lo, f_lo + nf_out)
   const CT scale = (CT)a.scale;
-  const bool amax = a.argmax != nullptr;
-  CT* out = reinterpret_cast<CT*>(a.out) + ((int64_t)slot * a.nt_out + fi) * a.nf_out;
   const int N = a.nfft;
   const cplx<CT>* post = reinterpret_cast<const cplx<CT>*>(a.post);
-  CT bv = -__builtin_huge_val();
-  int bi = 0x7fffffff;
-  for (int i = threadIdx.x; i < a.nf_out; i += kThreads) {
+  // the argument of the log for kept bin i: 1e-12 + |X|^2 / (sum w)^2
+  auto level = [&](int i) -> CT {
     const int k = a.f_lo + i;
     cplx<CT> X;
     if constexpr (CPLX) {
-      X = buf[k];
+      X = buf[pidx(k)];
     } else {
       const int kk = (k <= P) ? k : N - k;  // real signal: X[N-k] = conj X[k]
-      const cplx<CT> A = buf[kk == P ? 0 : kk];
-      const cplx<CT> Bc = buf[kk == 0 ? 0 : P - kk];
+      const cplx<CT> A = buf[pidx(kk == P ? 0 : kk)];
+      const cplx<CT> Bc = buf[pidx(kk == 0 ? 0 : P - kk)];
       const cplx<CT> B = {Bc.x, -Bc.y};
       const cplx<CT> s = cadd(A, B), d = csub(A, B);
       const cplx<CT> wd = cmul(post[kk], d);
@@ -305,31 +362,60 @@ __global__ __launch_bounds__(kThreads) void k_stft(StftArgs a) {
       X = {(CT)0.5 * (s.x + wd.y), (CT)0.5 * (s.y - wd.x)};
     }
     const CT pw = (X.x * X.x + X.y * X.y) * scale;
-    CT db;
-    if constexpr (sizeof(CT) == 4) {
-      const float v = 1e-12f + pw;
-      db = 10.0f * log10f(v);
-    } else {
-      db = 10.0 * log10(1e-12 + pw);
-    }
-    if (amax) {
+    return (CT)1e-12 + pw;
+  };
+  auto db_of = [](CT v) -> CT {
+    if constexpr (sizeof(CT) == 4) return 10.0f * log10f(v);
+    else return 10.0 * log10(v);
+  };
+  if (a.argmax == nullptr) {
+    CT* out = reinterpret_cast<CT*>(a.out) + ((int64_t)slot * a.nt_out + fi) * a.nf_out;
+    for (int i = threadIdx.x; i < a.nf_out; i += kThreads) out[i] = db_of(level(i));
+    return;
+  }
+  // argmax (np.argmax of the dB row).  The log is monotonic, so only bins whose level lies within
+  // rounding of the largest level can hold the largest dB value: pass 1 finds the largest level,
+  // pass 2 takes the log of the bins within a relative 1e-9 (float64; 1e-4 for float32, far above
+  // the log's few-ulp error) of it and compares their dB values exactly (first index on ties).
+  unsigned char* scratch = smem + (size_t)(P + P / 16 + 1) * sizeof(cplx<CT>);
+  CT* sv = reinterpret_cast<CT*>(scratch);
+  int* si = reinterpret_cast<int*>(scratch + sizeof(CT) * (kThreads / kWave));
+  const int w = threadIdx.x / kWave;
+  CT vm = -__builtin_huge_val();
+  int vi = 0x7fffffff;
+  for (int i = threadIdx.x; i < a.nf_out; i += kThreads) {
+    const CT v = level(i);
+    if (argmax_better(v, i, vm, vi)) { vm = v; vi = i; }
+  }
+#pragma unroll
+  for (int off = kWave / 2; off > 0; off >>= 1) {
+    const CT ov = __shfl_xor(vm, off);
+    const int oi = __shfl_xor(vi, off);
+    if (argmax_better(ov, oi, vm, vi)) { vm = ov; vi = oi; }
+  }
+  if ((threadIdx.x & (kWave - 1)) == 0) { sv[w] = vm; si[w] = vi; }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kThreads / kWave; ++k)
+    if (argmax_better(sv[k], si[k], vm, vi)) { vm = sv[k]; vi = si[k]; }
+  const bool vnan = vm != vm;
+  const CT thr = vm * (sizeof(CT) == 4 ? (CT)(1.0 - 1e-4) : (CT)(1.0 - 1e-9));
+  CT bv = -__builtin_huge_val();
+  int bi = 0x7fffffff;
+  for (int i = threadIdx.x; i < a.nf_out; i += kThreads) {
+    const CT v = level(i);
+    if (vnan ? (v != v) : (v >= thr)) {
+      const CT db = db_of(v);
       if (argmax_better(db, i, bv, bi)) { bv = db; bi = i; }
-    } else {
-      out[i] = db;
     }
   }
-  if (!amax) return;
-  // workgroup argmax: within each wave by shuffles, then across the waves through LDS
 #pragma unroll
   for (int off = kWave / 2; off > 0; off >>= 1) {
     const CT ov = __shfl_xor(bv, off);
     const int oi = __shfl_xor(bi, off);
     if (argmax_better(ov, oi, bv, bi)) { bv = ov; bi = oi; }
   }
-  __syncthreads();  // every thread is done reading the spectrum in buf
-  CT* sv = reinterpret_cast<CT*>(smem);
-  int* si = reinterpret_cast<int*>(smem + sizeof(CT) * (kThreads / kWave));
-  const int w = threadIdx.x / kWave;
+  __syncthreads();  // every thread has read sv / si of pass 1
   if ((threadIdx.x & (kWave - 1)) == 0) { sv[w] = bv; si[w] = bi; }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -573,10 +659,253 @@ __global__ __launch_bounds__(k38Threads) void k_stft3840(StftArgs a) {
   }
 }
 
+// ---- k_stftc3840: complex input, nfft = 3840, nperseg = 1920, hop = 240 M (M in 1, 2, 4, 8) -----
+// The beacon receiver's geometry (12 kHz complex baseband, frequency_correction.py; the reference
+// test runs steps_per_symbol = 8, hop 240).  P = 3840 = 16 x 16 x 15: 256 threads, one butterfly per
+// thread per stage, one padded LDS buffer.  Thread t < 240 owns the stage-1 inputs z[t + 240 r],
+// r < 8 (r >= 8 is the zero padding, so stage 1 is a half-input 16-point DFT); a frame advances by M
+// of those positions, so the thread keeps its 8 raw samples in registers and loads only M new ones
+// per frame (one at hop 240) -- every sample is read from HBM once -- prefetched while the current
+// frame is transformed.  Twiddles are powers of two per-thread seeds (recurrence); the stage-3 outputs
+// X[t + 256 r] come out in natural order in registers, so the epilogue (dB row or argmax) reads no
+// LDS.  Workgroups walk runs of kC38Chunk frames of one signal, runs of one signal on one XCD.
+constexpr int kC38P = 3840;
+constexpr int kC38Threads = 256;
+constexpr int kC38Chunk = 32;
+
+// 16-point DFT of a[0..7] with a[8..15] = 0 (4 x 4 Cooley-Tukey), in place, natural order
+template <typename T>
+__device__ __forceinline__ void dft16_half_t(cplx<T>* a) {
+  const T c1 = (T)0.92387953251128675613, s1 = (T)0.38268343236508977173, rr = (T)0.70710678118654752440;
+  const cplx<T> w[10] = {{(T)1, (T)0}, {c1, -s1}, {rr, -rr}, {s1, -c1}, {(T)0, (T)-1},
+                         {-s1, -c1}, {-rr, -rr}, {-c1, -s1}, {(T)-1, (T)0}, {-c1, s1}};
+  cplx<T> A[4][4];  // [n2][k1]
+#pragma unroll
+  for (int n2 = 0; n2 < 4; ++n2) {
+    const cplx<T> x0 = a[n2], x1 = a[4 + n2];
+    A[n2][0] = cadd(x0, x1);
+    A[n2][1] = cadd(x0, mul_mi(x1));
+    A[n2][2] = csub(x0, x1);
+    A[n2][3] = csub(x0, mul_mi(x1));
+  }
+#pragma unroll
+  for (int n2 = 1; n2 < 4; ++n2)
+#pragma unroll
+    for (int k1 = 1; k1 < 4; ++k1) A[n2][k1] = cmul(A[n2][k1], w[n2 * k1]);
+#pragma unroll
+  for (int k1 = 0; k1 < 4; ++k1) {
+    cplx<T> v[4] = {A[0][k1], A[1][k1], A[2][k1], A[3][k1]};
+    Dft<4, T>::run(v);
+#pragma unroll
+    for (int k2 = 0; k2 < 4; ++k2) a[k1 + 4 * k2] = v[k2];
+  }
+}
+
+template <typename InT, typename CT>
+__device__ __forceinline__ cplx<CT> load_c(const InT* x, int64_t n) {
+  if constexpr (sizeof(InT) == 8) {
+    const double2 v = *reinterpret_cast<const double2*>(x + 2 * n);
+    return {(CT)v.x, (CT)v.y};
+  } else {
+    const float2 v = *reinterpret_cast<const float2*>(x + 2 * n);
+    return {(CT)v.x, (CT)v.y};
+  }
+}
+
+template <typename InT, typename CT, int M>
+__global__ __launch_bounds__(kC38Threads, 2) void k_stftc3840(StftArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  cplx<CT>* buf = reinterpret_cast<cplx<CT>*>(smem);
+  CT* sv = reinterpret_cast<CT*>(smem + (size_t)(kC38P + kC38P / 16 + 1) * sizeof(cplx<CT>));
+  int* si = reinterpret_cast<int*>(sv + kC38Threads / kWave);
+  const int t = threadIdx.x;
+  const int w_id = t / kWave;
+  const int nt = a.nt_out;
+  const int chunks = (nt + kC38Chunk - 1) / kC38Chunk;
+  const int rr = (int)(blockIdx.x & 7) * a.per_xcd + (int)(blockIdx.x >> 3);
+  if (rr >= chunks * a.n_slots) return;
+  const int slot = rr / chunks, c = rr - slot * chunks;
+  const int f_begin = c * kC38Chunk, f_end = min(nt, f_begin + kC38Chunk);
+  const cplx<CT>* tw = reinterpret_cast<const cplx<CT>*>(a.tw);  // W_3840^m
+  const CT* win = reinterpret_cast<const CT*>(a.window);
+  const bool s1 = t < 240;
+  // twiddle seeds: stage 2 W_256^k = W_3840^(15 k) (k = t % 16), stage 3 W_3840^t; their powers are
+  // formed by complex recurrence each frame (relative error ~15 ulp, far inside the tolerances)
+  cplx<CT> s2 = tw[15 * (t & 15)], s3 = tw[t];
+  const InT* xs = reinterpret_cast<const InT*>(a.samples) + (int64_t)slot * a.slot_stride * 2;
+  cplx<CT> raw[8];
+  {
+    const int64_t base = (int64_t)(a.t_lo + f_begin) * a.hop;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) raw[r] = s1 ? load_c<InT, CT>(xs, base + t + 240 * r) : cplx<CT>{(CT)0, (CT)0};
+  }
+  const CT scale = (CT)a.scale;
+  const bool amax = a.argmax != nullptr;
+  const int k_lo = a.f_lo, k_hi = a.f_lo + a.nf_out;
+  for (int f = f_begin; f < f_end; ++f) {
+    // re-opaque the seeds so the per-frame twiddle powers are not hoisted into ~60 live registers
+    if constexpr (sizeof(CT) == 8) {
+      asm volatile("" : "+v"(s2.x), "+v"(s2.y), "+v"(s3.x), "+v"(s3.y));
+    } else {
+      asm volatile("" : "+v"(s2.x), "+v"(s2.y), "+v"(s3.x), "+v"(s3.y));
+    }
+    cplx<CT> nx[M];
+    const bool more = f + 1 < f_end;
+    if (s1 && more) {
+      const int64_t base = (int64_t)(a.t_lo + f + 1) * a.hop;
+#pragma unroll
+      for (int q = 0; q < M; ++q) nx[q] = load_c<InT, CT>(xs, base + t + 240 * (8 - M + q));
+    }
+    cplx<CT> v[16];
+    // stage 1: radix 16, Ns = 1 -> buf[16 t + k].  The window is re-read each frame (L1-resident;
+    // the opaque pointer keeps the 8 values from being hoisted into registers for the whole walk)
+    if (s1) {
+      const CT* wp = win;
+      asm volatile("" : "+s"(wp));
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const CT wv = wp[t + 240 * r];
+        v[r] = {wv * raw[r].x, wv * raw[r].y};
+      }
+      dft16_half_t<CT>(v);
+#pragma unroll
+      for (int k = 0; k < 16; ++k) buf[pidx(16 * t + k)] = v[k];
+    }
+    __syncthreads();
+    // stage 2: radix 16, Ns = 16: buf[t + 240 r] -> twiddle W_256^(r k), k = t % 16 -> buf[(t/16) 256 + k + 16 r]
+    if (s1) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v[r] = buf[pidx(t + 240 * r)];
+    }
+    __syncthreads();
+    if (s1) {
+      const int k = t & 15;
+      cplx<CT> wr = s2;
+#pragma unroll
+      for (int r = 1; r < 16; ++r) {
+        v[r] = cmul(v[r], wr);
+        wr = cmul(wr, s2);
+      }
+      Dft<16, CT>::run(v);
+      const int d0 = (t >> 4) * 256 + k;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) buf[pidx(d0 + 16 * r)] = v[r];
+    }
+    __syncthreads();
+    // stage 3: radix 15, Ns = 256: buf[t + 256 r] -> twiddle W_3840^(r t) -> X[t + 256 r]
+#pragma unroll
+    for (int r = 0; r < 15; ++r) v[r] = buf[pidx(t + 256 * r)];
+    __syncthreads();  // the next frame's stage 1 may overwrite buf
+    {
+      cplx<CT> wr = s3;
+#pragma unroll
+      for (int r = 1; r < 15; ++r) {
+        v[r] = cmul(v[r], wr);
+        wr = cmul(wr, s3);
+      }
+    }
+    Dft<15, CT>::run(v);
+    // epilogue on the registers: level = 1e-12 + |X|^2 / (sum w)^2 of kept bins
+    CT lv[15];
+#pragma unroll
+    for (int r = 0; r < 15; ++r) lv[r] = (CT)1e-12 + (v[r].x * v[r].x + v[r].y * v[r].y) * scale;
+    if (!amax) {
+      CT* out = reinterpret_cast<CT*>(a.out) + ((int64_t)slot * nt + f) * a.nf_out;
+#pragma unroll
+      for (int r = 0; r < 15; ++r) {
+        const int k = t + 256 * r;
+        if (k >= k_lo && k < k_hi) {
+          if constexpr (sizeof(CT) == 4) out[k - k_lo] = 10.0f * log10f(lv[r]);
+          else out[k - k_lo] = 10.0 * log10(lv[r]);
+        }
+      }
+    } else {
+      // two-pass argmax of the dB row (see k_stft): largest level, then exact dB near it
+      CT vm = -__builtin_huge_val();
+      int vi = 0x7fffffff;
+#pragma unroll
+      for (int r = 0; r < 15; ++r) {
+        const int k = t + 256 * r;
+        if (k >= k_lo && k < k_hi && argmax_better(lv[r], k, vm, vi)) { vm = lv[r]; vi = k; }
+      }
+#pragma unroll
+      for (int off = kWave / 2; off > 0; off >>= 1) {
+        const CT ov = __shfl_xor(vm, off);
+        const int oi = __shfl_xor(vi, off);
+        if (argmax_better(ov, oi, vm, vi)) { vm = ov; vi = oi; }
+      }
+      if ((t & (kWave - 1)) == 0) { sv[w_id] = vm; si[w_id] = vi; }
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < kC38Threads / kWave; ++k)
+        if (argmax_better(sv[k], si[k], vm, vi)) { vm = sv[k]; vi = si[k]; }
+      const bool vnan = vm != vm;
+      const CT thr = vm * (sizeof(CT) == 4 ? (CT)(1.0 - 1e-4) : (CT)(1.0 - 1e-9));
+      CT bv = -__builtin_huge_val();
+      int bi = 0x7fffffff;
+#pragma unroll
+      for (int r = 0; r < 15; ++r) {
+        const int k = t + 256 * r;
+        if (k >= k_lo && k < k_hi && (vnan ? (lv[r] != lv[r]) : (lv[r] >= thr))) {
+          CT db;
+          if constexpr (sizeof(CT) == 4) db = 10.0f * log10f(lv[r]);
+          else db = 10.0 * log10(lv[r]);
+          if (argmax_better(db, k, bv, bi)) { bv = db; bi = k; }
+        }
+      }
+#pragma unroll
+      for (int off = kWave / 2; off > 0; off >>= 1) {
+        const CT ov = __shfl_xor(bv, off);
+        const int oi = __shfl_xor(bi, off);
+        if (argmax_better(ov, oi, bv, bi)) { bv = ov; bi = oi; }
+      }
+      __syncthreads();  // pass-1 values read by every thread
+      if ((t & (kWave - 1)) == 0) { sv[w_id] = bv; si[w_id] = bi; }
+      __syncthreads();
+      if (t == 0) {
+        for (int k = 1; k < kC38Threads / kWave; ++k)
+          if (argmax_better(sv[k], si[k], bv, bi)) { bv = sv[k]; bi = si[k]; }
+        a.argmax[(int64_t)slot * nt + f] = bi - k_lo;
+      }
+    }
+    // slide the raw samples by M positions
+    if (more) {
+#pragma unroll
+      for (int r = 0; r < 8 - M; ++r) raw[r] = raw[r + M];
+#pragma unroll
+      for (int q = 0; q < M; ++q) raw[8 - M + q] = nx[q];
+    }
+  }
+}
+
+template <typename InT, typename CT>
+hipError_t launch_c3840(const StftLaunch& L, StftArgs a, hipStream_t s) {
+  const int chunks = (a.nt_out + kC38Chunk - 1) / kC38Chunk;
+  a.per_xcd = (int)(((int64_t)chunks * L.n_slots + 7) / 8);
+  const dim3 grid((unsigned)(8 * a.per_xcd));
+  const size_t lds = (size_t)(kC38P + kC38P / 16 + 1) * sizeof(cplx<CT>) + 64;
+  auto go = [&](auto kern) {
+    if (lds > 64 * 1024) {
+      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(kern, grid, dim3(kC38Threads), lds, s, a);
+    return hipGetLastError();
+  };
+  switch (L.hop) {
+    case 240: return go(k_stftc3840<InT, CT, 1>);
+    case 480: return go(k_stftc3840<InT, CT, 2>);
+    case 960: return go(k_stftc3840<InT, CT, 4>);
+    default: return go(k_stftc3840<InT, CT, 8>);
+  }
+}
+
 template <typename InT, bool CPLX, typename CT>
 hipError_t launch_t(const StftLaunch& L, const StftArgs& a, hipStream_t s) {
   const dim3 grid((unsigned)(8 * a.per_xcd));  // see k_stft: a.per_xcd (slot, frame) pairs per XCD
-  const size_t lds = (size_t)a.P * sizeof(cplx<CT>);
+  // pidx padding + the argmax epilogue's cross-wave scratch
+  const size_t lds = (size_t)(a.P + a.P / 16 + 1) * sizeof(cplx<CT>) + 64;
   auto go = [&](auto kern) {
     if (lds > 64 * 1024) {
       hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
@@ -587,6 +916,9 @@ hipError_t launch_t(const StftLaunch& L, const StftArgs& a, hipStream_t s) {
     return hipGetLastError();
   };
   if (a.P <= kThreads * 8) return go(k_stft<InT, CPLX, CT, 8>);
+  // P <= 3840 (3840 = 16 x 16 x 15: one butterfly per thread per stage) keeps half the registers
+  // of the P <= 4096 variant, whose radix-15 stage would hold two butterflies per thread
+  if (a.P <= kThreads * 15) return go(k_stft<InT, CPLX, CT, 15>);
   if (a.P <= kThreads * 16) return go(k_stft<InT, CPLX, CT, 16>);
   return go(k_stft<InT, CPLX, CT, 32>);
 }
@@ -624,6 +956,12 @@ hipError_t launch_stft(const StftLaunch& L, hipStream_t s) {
     if (L.dtype == FT8_F32) hipLaunchKernelGGL(k_stft3840<float>, grid, dim3(k38Threads), 0, s, a);
     else hipLaunchKernelGGL(k_stft3840<int16_t>, grid, dim3(k38Threads), 0, s, a);
     return hipGetLastError();
+  }
+  // complex input in the beacon receiver's geometry (12 kHz: nfft 3840, nperseg 1920, hop 240 M)
+  if ((L.dtype == FT8_C64 || L.dtype == FT8_C128) && L.nfft == kC38P && L.nperseg == 1920 && a.P == kC38P &&
+      (L.hop == 240 || L.hop == 480 || L.hop == 960 || L.hop == 1920)) {
+    if (L.dtype == FT8_C128) return launch_c3840<double, double>(L, a, s);
+    return launch_c3840<float, float>(L, a, s);
   }
   switch (L.dtype) {
     case FT8_F32: return launch_t<float, false, float>(L, a, s);
