@@ -505,7 +505,9 @@ __device__ __forceinline__ void load_pair(const InT* x, int64_t n0, float& a, fl
 
 template <typename InT>
 __global__ __launch_bounds__(k38Threads) void k_stft3840(StftArgs a) {
-  __shared__ cplx<float> bufA[k38P];
+  // bufA is read and written with pidx padding: the stage-1 writes go out with a 16-complex stride
+  // across lanes (128 B: 32-way bank conflicts unpadded)
+  __shared__ cplx<float> bufA[k38P + k38P / 16 + 1];
   __shared__ cplx<float> bufB[k38P];
   const int t = threadIdx.x;
   const int chunks = (a.nt_out + k38Chunk - 1) / k38Chunk;
@@ -565,7 +567,7 @@ __global__ __launch_bounds__(k38Threads) void k_stft3840(StftArgs a) {
       for (int r = 0; r < 8; ++r) z[r] = {w0[r] * ra[r], w1[r] * rb[r]};
       dft16_half(z, y);
 #pragma unroll
-      for (int k = 0; k < 16; ++k) bufA[16 * t + k] = y[k];
+      for (int k = 0; k < 16; ++k) bufA[pidx(16 * t + k)] = y[k];
     }
     __syncthreads();
     // stage 2: radix 8, Ns = 16: j in {t, t + 128} (j < 240)
@@ -575,7 +577,7 @@ __global__ __launch_bounds__(k38Threads) void k_stft3840(StftArgs a) {
       if (j < 240) {
         cplx<float> v[8];
 #pragma unroll
-        for (int r = 0; r < 8; ++r) v[r] = bufA[j + 240 * r];
+        for (int r = 0; r < 8; ++r) v[r] = bufA[pidx(j + 240 * r)];
         if ((j & 15) != 0) {
           cplx<float> w = s2;  // W_128^(r k)
 #pragma unroll
@@ -606,7 +608,7 @@ __global__ __launch_bounds__(k38Threads) void k_stft3840(StftArgs a) {
       }
       dft15(v, y);
 #pragma unroll
-      for (int r = 0; r < 15; ++r) bufA[t + 128 * r] = y[r];
+      for (int r = 0; r < 15; ++r) bufA[pidx(t + 128 * r)] = y[r];
     }
     __syncthreads();
     // epilogue: real-signal spectrum, power, dB, kept bins
@@ -617,8 +619,8 @@ __global__ __launch_bounds__(k38Threads) void k_stft3840(StftArgs a) {
       // d = Z[k] - conj Z[P-k]
       cplx<float> pw_k = p0;  // W_3840^k, k = t + 128 j
       for (int k = t; k <= k38P / 2; k += k38Threads) {
-        const cplx<float> A = bufA[k];
-        const cplx<float> Bc = bufA[k == 0 ? 0 : k38P - k];
+        const cplx<float> A = bufA[pidx(k)];
+        const cplx<float> Bc = bufA[pidx(k == 0 ? 0 : k38P - k)];
         const cplx<float> B = {Bc.x, -Bc.y};
         const cplx<float> sm = cadd(A, B), df = csub(A, B);
         const cplx<float> wd = cmul(pw_k, df);
@@ -635,8 +637,8 @@ __global__ __launch_bounds__(k38Threads) void k_stft3840(StftArgs a) {
       for (int i = t; i < a.nf_out; i += k38Threads) {
         const int k = a.f_lo + i;
         const int kk = (k <= k38P) ? k : 2 * k38P - k;
-        const cplx<float> A = bufA[kk == k38P ? 0 : kk];
-        const cplx<float> Bc = bufA[kk == 0 ? 0 : k38P - kk];
+        const cplx<float> A = bufA[pidx(kk == k38P ? 0 : kk)];
+        const cplx<float> Bc = bufA[pidx(kk == 0 ? 0 : k38P - kk)];
         const cplx<float> B = {Bc.x, -Bc.y};
         const cplx<float> sm = cadd(A, B), df = csub(A, B);
         const cplx<float> wd = cmul(rec_post ? pw_k : post[kk], df);
