@@ -258,13 +258,17 @@ int get_plan(ft8_ctx* c, int nfft, bool cplx, bool f64, FftPlan* out) {
   e.nfft = nfft;
   e.cplx = cplx;
   e.f64 = f64;
-  const int P = cplx ? nfft : nfft / 2;
-  if (!cplx && (nfft % 2)) return fail(c, FT8_E_UNSUPPORTED, "odd nfft is not supported for real input");
-  if (P > (cplx ? kMaxFftComplex : kMaxFftReal / 2))
-    return fail(c, FT8_E_RANGE, "nfft " + std::to_string(nfft) + " exceeds the compiled FFT limit");
+  int P = cplx ? nfft : nfft / 2;
+  e.plan.dft = 0;
+  // lengths the LDS Stockham FFT cannot take (a prime factor above 7, odd real nfft, above the
+  // compiled limit) fall back to the direct DFT kernel: P = nfft, tw = W_nfft^m
+  if ((!cplx && (nfft % 2)) || P > (cplx ? kMaxFftComplex : kMaxFftReal / 2) || !factor(P, e.plan)) {
+    if (nfft > kMaxDft) return fail(c, FT8_E_RANGE, "nfft " + std::to_string(nfft) + " exceeds the compiled DFT limit");
+    P = nfft;
+    e.plan.dft = 1;
+    e.plan.nstages = 0;
+  }
   e.plan.P = P;
-  if (!factor(P, e.plan))
-    return fail(c, FT8_E_UNSUPPORTED, "FFT length " + std::to_string(P) + " has a prime factor other than 2,3,5,7");
   // twiddles W_P^m and post-processing W_N^k (N = 2P), from long double angles
   const size_t esz = f64 ? 16 : 8;
   std::vector<unsigned char> tw(esz * P), post(esz * (P + 1));
@@ -328,6 +332,8 @@ int do_stft(ft8_ctx* c, const void* samples, int dtype, int64_t n_samples, int n
   StftLaunch L{};
   rc = get_plan(c, g.nfft, cplx, f64, &L.plan);
   if (rc) return rc;
+  if (L.plan.dft && (size_t)g.nperseg * (f64 ? 16 : 8) > (size_t)kMaxDftLds)
+    return fail(c, FT8_E_RANGE, "nperseg " + std::to_string(g.nperseg) + " exceeds the direct-DFT limit");
   WinEntry* w = nullptr;
   rc = get_window(c, g.nperseg, f64, &w);
   if (rc) return rc;
@@ -658,6 +664,14 @@ int stft_argmax_core(ft8_ctx* c, const void* x, int dtype, int64_t n_samples, in
   const bool f64 = is_f64_dtype(dtype), cplx = is_cplx_dtype(dtype);
   StftLaunch L{};
   if ((rc = get_plan(c, g.nfft, cplx, f64, &L.plan))) return rc;
+  if (L.plan.dft) {
+    // the direct DFT writes the dB rows, then reduces each to its argmax: stage them in wf
+    if ((size_t)g.nperseg * (f64 ? 16 : 8) > (size_t)kMaxDftLds)
+      return fail(c, FT8_E_RANGE, "nperseg " + std::to_string(g.nperseg) + " exceeds the direct-DFT limit");
+    const size_t bytes = (size_t)n_slots * (p->t_hi - p->t_lo) * (p->f_hi - p->f_lo) * (f64 ? 8 : 4);
+    if ((rc = ensure(c, c->wf, bytes))) return rc;
+    L.out = c->wf.p;
+  }
   WinEntry* w = nullptr;
   if ((rc = get_window(c, g.nperseg, f64, &w))) return rc;
   L.samples = x;

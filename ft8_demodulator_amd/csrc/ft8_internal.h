@@ -13,6 +13,8 @@ constexpr int kWave = 64;
 constexpr int kMaxCandidates = 4096;   // LDS-resident selection (k_select)
 constexpr int kMaxFftReal = 16384;     // nfft of the real-input path (half-length FFT <= 8192)
 constexpr int kMaxFftComplex = 8192;   // nfft of the complex-input path
+constexpr int kMaxDft = 1 << 18;       // nfft of the direct-DFT fallback (any factorisation)
+constexpr int kMaxDftLds = 150 * 1024; // its windowed frame is staged in LDS
 
 __host__ __device__ inline int floordiv(int a, int b) {
   int q = a / b;
@@ -27,7 +29,8 @@ struct cplx {
 
 // ---- STFT plan (host-built tables, device-resident) ----------------------------------------
 struct FftPlan {
-  int P;              // transform length (nfft/2 for real input, nfft for complex input)
+  int P;              // transform length (nfft/2 for real input, nfft for complex input; nfft if dft)
+  int dft;            // 1: no 2/3/5/7 factorisation (or odd real nfft): direct DFT, tw = W_nfft^m
   int nstages;
   int radix[16];
   const void* tw;     // W_P^m, m in [0, P): cplx<float> or cplx<double>
@@ -45,6 +48,7 @@ struct StftLaunch {
   double scale;            // 1 / (sum w)^2
   void* out;               // float or double [n_slots][t_hi-t_lo][f_hi-f_lo]
   int32_t* argmax;         // non-null: write per-frame argmax over the kept bins instead of `out`
+                           // (a direct-DFT plan then writes the dB rows to `out` first)
   FftPlan plan;
 };
 hipError_t launch_stft(const StftLaunch& a, hipStream_t s);

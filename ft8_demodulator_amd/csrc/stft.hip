@@ -903,6 +903,100 @@ hipError_t launch_c3840(const StftLaunch& L, StftArgs a, hipStream_t s) {
   }
 }
 
+// ---- k_stft_dft: direct DFT for lengths the FFT plans cannot take ---------------------------
+// (a prime factor above 7, e.g. 32 768 Hz: nfft = 10 485 = 3 x 5 x 3 x 233; odd real nfft; nfft
+// above the LDS FFT limit).  One workgroup per (bin block of 256, frame, slot): the windowed frame
+// is staged in LDS, each thread sums its bin X[k] = sum_n z[n] W^(k n) sequentially in n, the twiddle
+// advanced by complex recurrence and re-seeded from the exact table entry W^((k n) mod nfft) every
+// 32 samples.  A fallback for correctness on any geometry, O(nperseg) work per bin.
+constexpr int kDftThreads = 256;
+constexpr int kDftReseed = 32;
+
+template <typename InT, bool CPLX, typename CT>
+__global__ __launch_bounds__(kDftThreads) void k_stft_dft(StftArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  cplx<CT>* z = reinterpret_cast<cplx<CT>*>(smem);
+  const int nbb = (a.nf_out + kDftThreads - 1) / kDftThreads;
+  const int fi = blockIdx.x / nbb, bb = blockIdx.x - fi * nbb;
+  const int slot = blockIdx.y;
+  const int frame = a.t_lo + fi;
+  const InT* xs = reinterpret_cast<const InT*>(a.samples) +
+                  (int64_t)slot * a.slot_stride * (CPLX ? 2 : 1) + (int64_t)frame * a.hop * (CPLX ? 2 : 1);
+  const CT* win = reinterpret_cast<const CT*>(a.window);
+  const int L = a.nperseg, N = a.nfft;
+  for (int n = threadIdx.x; n < L; n += kDftThreads) {
+    CT re, im = (CT)0;
+    if constexpr (CPLX) {
+      re = (CT)xs[2 * n];
+      im = (CT)xs[2 * n + 1];
+    } else if constexpr (sizeof(CT) == 4) {
+      re = load_f32<InT>(xs, n);
+    } else {
+      re = (CT)xs[n];
+    }
+    z[n] = {win[n] * re, win[n] * im};
+  }
+  __syncthreads();
+  const int i = bb * kDftThreads + threadIdx.x;
+  if (i >= a.nf_out) return;
+  const int k = a.f_lo + i;
+  const cplx<CT>* tw = reinterpret_cast<const cplx<CT>*>(a.tw);  // W_N^m, m in [0, N)
+  const cplx<CT> step = tw[k % N];
+  cplx<CT> acc = {(CT)0, (CT)0};
+  for (int n0 = 0; n0 < L; n0 += kDftReseed) {
+    cplx<CT> w = tw[(int)(((int64_t)k * n0) % N)];
+    const int n1 = min(L, n0 + kDftReseed);
+    for (int n = n0; n < n1; ++n) {
+      const cplx<CT> v = cmul(z[n], w);
+      acc = cadd(acc, v);
+      w = cmul(w, step);
+    }
+  }
+  const CT pw = (acc.x * acc.x + acc.y * acc.y) * (CT)a.scale;
+  CT* out = reinterpret_cast<CT*>(a.out) + ((int64_t)slot * a.nt_out + fi) * a.nf_out;
+  if constexpr (sizeof(CT) == 4) out[i] = 10.0f * log10f(1e-12f + pw);
+  else out[i] = 10.0 * log10(1e-12 + pw);
+}
+
+// np.argmax of each dB row [slot][frame][nf] (the direct-DFT path's argmax): one wave per row
+template <typename CT>
+__global__ __launch_bounds__(kWave) void k_row_argmax(const CT* rows, int nf, int64_t n_rows, int32_t* idx) {
+  const int64_t r = blockIdx.x;
+  if (r >= n_rows) return;
+  const CT* row = rows + r * nf;
+  CT bv = -__builtin_huge_val();
+  int bi = 0x7fffffff;
+  for (int i = threadIdx.x; i < nf; i += kWave)
+    if (argmax_better(row[i], i, bv, bi)) { bv = row[i]; bi = i; }
+#pragma unroll
+  for (int off = kWave / 2; off > 0; off >>= 1) {
+    const CT ov = __shfl_xor(bv, off);
+    const int oi = __shfl_xor(bi, off);
+    if (argmax_better(ov, oi, bv, bi)) { bv = ov; bi = oi; }
+  }
+  if (threadIdx.x == 0) idx[r] = bi;
+}
+
+template <typename InT, bool CPLX, typename CT>
+hipError_t launch_dft(const StftLaunch& L, const StftArgs& a, hipStream_t s) {
+  const size_t lds = (size_t)L.nperseg * sizeof(cplx<CT>);
+  if (lds > (size_t)kMaxDftLds) return hipErrorInvalidValue;
+  auto kern = k_stft_dft<InT, CPLX, CT>;
+  if (lds > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  const int nbb = (a.nf_out + kDftThreads - 1) / kDftThreads;
+  hipLaunchKernelGGL(kern, dim3((unsigned)(nbb * a.nt_out), (unsigned)L.n_slots), dim3(kDftThreads), lds, s, a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || !L.argmax) return e;
+  const int64_t rows = (int64_t)a.nt_out * L.n_slots;
+  hipLaunchKernelGGL(k_row_argmax<CT>, dim3((unsigned)rows), dim3(kWave), 0, s, reinterpret_cast<const CT*>(a.out),
+                     a.nf_out, rows, L.argmax);
+  return hipGetLastError();
+}
+
 template <typename InT, bool CPLX, typename CT>
 hipError_t launch_t(const StftLaunch& L, const StftArgs& a, hipStream_t s) {
   const dim3 grid((unsigned)(8 * a.per_xcd));  // see k_stft: a.per_xcd (slot, frame) pairs per XCD
@@ -950,6 +1044,17 @@ hipError_t launch_stft(const StftLaunch& L, hipStream_t s) {
   a.n_slots = L.n_slots;
   a.per_xcd = (int)(((int64_t)a.nt_out * L.n_slots + 7) / 8);
   if (a.nt_out <= 0 || a.nf_out <= 0 || L.n_slots <= 0) return hipSuccess;
+  if (L.plan.dft) {
+    a.argmax = nullptr;  // the DFT kernel writes dB rows; launch_dft reduces them to the argmax
+    switch (L.dtype) {
+      case FT8_F32: return launch_dft<float, false, float>(L, a, s);
+      case FT8_I16: return launch_dft<int16_t, false, float>(L, a, s);
+      case FT8_F64: return launch_dft<double, false, double>(L, a, s);
+      case FT8_C64: return launch_dft<float, true, float>(L, a, s);
+      case FT8_C128: return launch_dft<double, true, double>(L, a, s);
+      default: return hipErrorInvalidValue;
+    }
+  }
   // production geometry: 12 kHz, bins_per_tone = steps_per_symbol = 2 (pairs need an even stride)
   if (!L.argmax && (L.dtype == FT8_F32 || L.dtype == FT8_I16) && L.nfft == 2 * k38P && L.nperseg == k38P && L.hop == 960 &&
       a.P == k38P && (L.slot_stride % 2) == 0) {

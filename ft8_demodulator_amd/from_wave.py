@@ -58,10 +58,12 @@ def decode_ft8_from_wave(wave_path: str, freq_min: float = None, freq_max: float
                          correction: bool = False, device=None, verbose: bool = False) -> list:
     """from_wave.py:71-178."""
     if correction:
-        # from_wave.py:105-159 -> frequency_correction.correct_frequency_drift: out of scope for this
-        # build (SURVEY.md section 8f); the reference path raises TypeError at
-        # frequency_correction.py:164-166 anyway.
-        raise NotImplementedError("frequency-drift correction is not part of the GPU receive path")
+        # from_wave.py:105-159 passes an FT8Waterfall as correct_frequency_drift's `params`, whose
+        # default filling (frequency_correction.py:164-166) raises TypeError: the reference CLI's
+        # correction path never decodes.  Same error here; the correction itself is available as
+        # ft8_demodulator_amd.frequency_correction.correct_frequency_drift (GPU).
+        raise TypeError("argument of type 'FT8Waterfall' is not iterable "
+                        "(from_wave.py:152-158 passes a waterfall as correct_frequency_drift's params)")
     data, dtype, sample_rate = _read_raw(wave_path, verbose)
     if dtype == np.int16:
         import torch

@@ -37,7 +37,7 @@ enum ft8_status {
   FT8_OK = 0,
   FT8_E_ARG = -1,         /* invalid argument (message in ft8_last_error) */
   FT8_E_HIP = -2,         /* HIP runtime error */
-  FT8_E_UNSUPPORTED = -3, /* e.g. an FFT length with a prime factor other than 2,3,5,7 */
+  FT8_E_UNSUPPORTED = -3, /* an input the path does not take (e.g. a dtype a stage does not accept) */
   FT8_E_NOMEM = -4,       /* device allocation failed */
   FT8_E_RANGE = -5        /* a size exceeds a compiled limit (see ft8_limits) */
 };

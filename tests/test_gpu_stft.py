@@ -30,3 +30,29 @@ def test_short_input_empty(gpu):
     from ft8_demodulator_amd import calculate_spectrogram
     s, f, t = calculate_spectrogram(np.zeros(10), 12000)
     assert s.shape == (1, 0) and f.size == 0 and t.size == 0
+
+
+@pytest.mark.parametrize("fs,bpt,sps,cplx,dt", [
+    (32768, 2, 2, False, np.float64),   # nfft 10485: odd and a prime factor 233 (reference test rate)
+    (32768, 2, 8, True, np.complex128),
+    (11025, 3, 2, False, np.float32),   # nfft 5292 = 2^2 3^3 7^2 ... P = 2646 = 2 3^3 7^2: FFT path
+    (9973, 1, 2, False, np.float32),    # prime-ish rate: nfft 1595 = 5 x 11 x 29, odd real
+])
+def test_any_fft_length_matches_scipy(gpu, oracle, fs, bpt, sps, cplx, dt):
+    """Lengths without a 2/3/5/7 factorisation (or odd real nfft) take the direct-DFT kernel; every
+    geometry matches scipy within the same tolerances as the golden cases."""
+    from ft8_demodulator_amd import calculate_spectrogram
+    rng = np.random.default_rng(fs + sps)
+    n = int(0.16 * fs) * 12
+    x = rng.normal(size=n) + (1j * rng.normal(size=n) if cplx else 0)
+    x = x + 3 * np.exp(2j * np.pi * 1000.0 * np.arange(n) / fs) if cplx else x + 3 * np.cos(2 * np.pi * 1000.0 * np.arange(n) / fs)
+    x = x.astype(dt)
+    spec, f, t = calculate_spectrogram(x, fs, bpt, sps)
+    ref, fr, tr = oracle.calculate_spectrogram(x, fs, bpt, sps)
+    assert spec.dtype == ref.dtype and spec.shape == ref.shape
+    assert np.array_equal(f, fr) and np.array_equal(t, tr)
+    strong = ref >= (ref.max(axis=0, keepdims=True) - 60.0)
+    d = np.abs(spec.astype(np.float64) - ref.astype(np.float64))
+    tight, loose = (1e-3, 0.25) if ref.dtype == np.float32 else (1e-6, 1e-3)
+    assert d[strong].max() <= tight, d[strong].max()
+    assert d.max() <= loose, d.max()

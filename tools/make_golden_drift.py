@@ -59,6 +59,10 @@ CASES = [
      {"bins_per_tone": 2, "steps_per_symbol": 8}),
     ("fs12k_noise_only", "1c3f8a6ae207a1e39451", 12000, 300.0, 500.0, 100.0, -60.0, 18,
      {"bins_per_tone": 2, "steps_per_symbol": 8}),
+    # the reference test's own configuration (test_correction.py:121-147): 32 768 Hz, 568 Hz/s,
+    # correction at steps_per_symbol 8 -> nfft 10 485 = 3 x 5 x 3 x 233 (the direct-DFT path)
+    ("fs32k_reference_test", "1c3f8a6ae207a1e39451", 32768, 300.0, 500.0, 568.0, 28.0, 19,
+     {"bins_per_tone": 2, "steps_per_symbol": 8}),
 ]
 
 
