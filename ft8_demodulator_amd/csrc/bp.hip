@@ -13,7 +13,7 @@
 //                sqrt(24/var) is correctly rounded, so LLRs are bit-identical to the reference.
 //   BP           bp_decode (ldpc_decoder.py:54-113) in float64, edge-parallel: the 522 Tanner-graph
 //                edges are dealt to lanes (9 per lane); variable->check and check->variable
-//                messages live in LDS (tov, toc: 2 x 4.2 KB) and every sum/product is evaluated in
+//                messages live in LDS (one 4.6 KB array, see WaveLds) and every sum/product is evaluated in
 //                the reference's order, without FMA contraction (-ffp-contract=off), so hard
 //                decisions match bit for bit.
 //   CRC          pack_bits + extract_crc + compute_crc (ft8_decode.py:200-273, crc.py:11-54).
@@ -159,23 +159,36 @@ __device__ __forceinline__ void div_rn(double* q, const double* x, const double*
 }
 
 // One LDS array holds both message sets: a sweep phase loads everything it needs before it stores
-// (the workgroup is one lockstep wave), so toc can overwrite tov in place and vice versa.  Edge
-// position e lives at msg[2e]; msg[2e + 1] is a constant 1.0, which stands in for the missing sixth
-// product factor of a degree-6 check (the companion of its position 5).
+// (the workgroup is one lockstep wave), so toc can overwrite tov in place and vice versa.
+//
+// Dense blocked layout (576 float64 = 9 slots of 64 lanes): the 83 check rows are packed first-fit
+// in check order into 18 blocks of 32 positions, rows never straddling a block; position 31 of
+// every block (lanes 31 and 63 of every slot) holds a constant 1.0, the missing sixth product
+// factor of the degree-6 rows of that block; the 36 unused positions are padding.  Messages are 8
+// bytes apart, so the edge-major loads and stores use all 64 LDS banks (the former interleaved
+// layout, edge e at msg[2e] beside a 1.0, used half of them).  The constant lanes never store; the
+// padding positions' cv entries point at a constant row (product 1.0), so every value a division
+// sees stays finite and non-zero.
 constexpr int kZeroBit = 255;  // bits[255] is never written: the padding checks' variable
+constexpr int kBlocks = kEdgePad / 32;   // 18
+constexpr int kPoffD7 = 0;               // poff[q]: degree-7 row, edge at row position q
+constexpr int kPoffD6 = 7;               // poff[7 + 31 q + rb]: degree-6 row starting rb into its block
+constexpr int kPoffOne = 7 + 31 * 6;     // all-zero offsets: six reads of the same 1.0
+constexpr int kPoffN = kPoffOne + 1;
 struct WaveLds {
-  double msg[2 * (kEdgePad + 8)];  // tov between sweeps; V->C arguments, then toc, within a sweep
-  uint64_t poff[16];               // [k + 7 * (degree == 6)]: byte offsets of the 6 product factors
+  double msg[kEdgePad];            // tov between sweeps; V->C arguments, then toc, within a sweep
+  uint64_t poff[kPoffN];           // byte offsets of the 6 product factors from the row base
   uint8_t bits[256];               // hard decision of every variable (last evaluated sweep)
   uint8_t a91[16];
 };
+static_assert(kEdgePad == 576 && kBlocks == 18, "blocked message layout assumes 9 edge slots");
 
 // Per-lane tables (registers, loaded once per wave).  A sweep runs in two layouts:
 //   variable-major (3 slots, variable n = lane + 64 j): hard decision and variable->check sums
 //     va: LDS byte address of the variable's 1st edge message | 2nd edge << 16 (check order)
 //     vb: LDS byte address of its 3rd edge message
-//   edge-major (9 slots, edge e = lane + 64 i): fast_tanh, check products, fast_atanh
-//     cv: LDS byte address of the check's row (&msg[2 * start]) | LDS address of its poff entry << 16
+//   edge-major (9 slots, position p = lane + 64 i): fast_tanh, check products, fast_atanh
+//     cv: LDS byte address of the row base | LDS address of its poff entry << 16
 //   check-major (2 slots, check m = lane + 64 k): parity
 //     pk: the check's variables, one byte each (7; a degree-6 check's 7th is kZeroBit)
 struct WaveTables {
@@ -189,46 +202,62 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
   return (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const void*)p;
 }
 
-// poff[k + 7 * d6] byte f = 16 * (row position of product factor f of the edge at row position k):
-// positions f + (f >= k), ascending (the reference's row order); a degree-6 check's sixth factor
-// is the 1.0 companion of position 5.
-__device__ void init_poff(WaveLds& L, int lane) {
-  if (lane < 14) {
-    const int k = lane % 7, d6 = lane >= 7;
-    uint64_t w = 0;
-    for (int f = 0; f < 6; ++f) {
-      const uint64_t b = (d6 && f == 5) ? 16 * 5 + 8 : 16 * (f + (f >= k));
-      w |= b << (8 * f);
-    }
-    L.poff[lane] = w;
-  }
-}
+__device__ __forceinline__ bool const_pos(int p) { return (p & 31) == 31; }
 
-__device__ void load_tables(WaveTables& t, const WaveLds& L, int lane) {
+// Builds the per-lane tables, the poff entries and the mask of this lane's padding positions
+// (bit i: position lane + 64 i).  The msg array serves as scratch for the row layout first.
+__device__ uint32_t load_tables(WaveTables& t, WaveLds& L, int lane) {
+  int16_t* rowpos = reinterpret_cast<int16_t*>(&L.msg[0]);            // [83] row start position
+  int16_t* pos2edge = reinterpret_cast<int16_t*>(&L.msg[0]) + 128;    // [576] edge at position, -1
+  if (lane == 0) {  // first fit in check order: 18 blocks of 31 usable positions
+    int fill[kBlocks];
+    for (int b = 0; b < kBlocks; ++b) fill[b] = 0;
+    for (int m = 0; m < FT8_LDPC_M; ++m) {
+      const int d = kChkStartD[m + 1] - kChkStartD[m];
+      int b = 0;
+      while (fill[b] + d > 31) ++b;  // always found: the packing of the FT8 code fits 18 blocks
+      rowpos[m] = (int16_t)(32 * b + fill[b]);
+      fill[b] += d;
+    }
+  }
+  for (int p = lane; p < kEdgePad; p += kWave) pos2edge[p] = -1;
+  __syncthreads();
+  for (int e = lane; e < FT8_LDPC_E; e += kWave) {
+    const int m = kEdgeChkD[e];
+    pos2edge[rowpos[m] + (e - kChkStartD[m])] = (int16_t)e;
+  }
+  __syncthreads();
   const uint32_t msg0 = lds_addr(&L.msg[0]), poff0 = lds_addr(&L.poff[0]);
-  const uint32_t dummy = msg0 + 16u * (kEdgePad - 1);  // padding variables use a padding edge
+  const uint32_t one = msg0 + 8u * 31u;  // a constant 1.0
+  auto pos_of = [&](int e) -> uint32_t {
+    const int m = kEdgeChkD[e];
+    return (uint32_t)(rowpos[m] + (e - kChkStartD[m]));
+  };
 #pragma unroll
   for (int j = 0; j < kVarSlots; ++j) {
     const int n = lane + kWave * j;
     if (n < FT8_LDPC_N) {
-      t.va[j] = (msg0 + 16u * kVarEdgeD[3 * n]) | ((msg0 + 16u * kVarEdgeD[3 * n + 1]) << 16);
-      t.vb[j] = msg0 + 16u * kVarEdgeD[3 * n + 2];
-    } else {
-      t.va[j] = dummy | (dummy << 16);
-      t.vb[j] = dummy;
+      t.va[j] = (msg0 + 8u * pos_of(kVarEdgeD[3 * n])) | ((msg0 + 8u * pos_of(kVarEdgeD[3 * n + 1])) << 16);
+      t.vb[j] = msg0 + 8u * pos_of(kVarEdgeD[3 * n + 2]);
+    } else {  // padding variable: reads the constant, never stores (see the sweep)
+      t.va[j] = one | (one << 16);
+      t.vb[j] = one;
     }
   }
+  uint32_t padmask = 0;
 #pragma unroll
   for (int i = 0; i < kEdgeSlots; ++i) {
-    const int e = lane + kWave * i;
-    if (e < FT8_LDPC_E) {
+    const int p = lane + kWave * i;
+    const int e = pos2edge[p];
+    if (e >= 0) {
       const int m = kEdgeChkD[e];
       const int s = kChkStartD[m], d = kChkStartD[m + 1] - s;
-      const uint32_t entry = (uint32_t)(e - s) + (d == 6 ? 7u : 0u);
-      t.cv[i] = (msg0 + 16u * (uint32_t)s) | ((poff0 + 8u * entry) << 16);
-    } else {  // padding edge: its check is the padding block at 522
-      const uint32_t k = (uint32_t)(e - FT8_LDPC_E) % 7u;
-      t.cv[i] = (msg0 + 16u * (uint32_t)FT8_LDPC_E) | ((poff0 + 8u * k) << 16);
+      const int r = rowpos[m], q = e - s;
+      const uint32_t entry = d == 7 ? (uint32_t)(kPoffD7 + q) : (uint32_t)(kPoffD6 + 31 * q + (r & 31));
+      t.cv[i] = (msg0 + 8u * (uint32_t)r) | ((poff0 + 8u * entry) << 16);
+    } else {
+      t.cv[i] = one | ((poff0 + 8u * kPoffOne) << 16);
+      if (!const_pos(p)) padmask |= 1u << i;
     }
   }
 #pragma unroll
@@ -246,6 +275,23 @@ __device__ void load_tables(WaveTables& t, const WaveLds& L, int lane) {
     t.pk[k][0] = w[0];
     t.pk[k][1] = w[1];
   }
+  // poff entries: byte f = 8 * (row position of product factor f): positions f + (f >= q) in row
+  // order; a degree-6 row's sixth factor is its block's constant at 31 - rb positions from the base
+  for (int x = lane; x < kPoffN; x += kWave) {
+    uint64_t w = 0;
+    if (x < kPoffD6) {
+      const int q = x;
+      for (int f = 0; f < 6; ++f) w |= (uint64_t)(8 * (f + (f >= q))) << (8 * f);
+    } else if (x < kPoffOne) {
+      const int q = (x - kPoffD6) / 31, rb = (x - kPoffD6) % 31;
+      for (int f = 0; f < 6; ++f) {
+        const int off = f == 5 ? 8 * (31 - rb) : 8 * (f + (f >= q));
+        w |= (uint64_t)off << (8 * f);
+      }
+    }
+    L.poff[x] = w;
+  }
+  __syncthreads();  // scratch reads done before the caller initialises msg
   // keep the tables in registers: opaque values cannot be rematerialised from memory in the loop
 #pragma unroll
   for (int j = 0; j < kVarSlots; ++j) asm volatile("" : "+v"(t.va[j]), "+v"(t.vb[j]));
@@ -253,6 +299,7 @@ __device__ void load_tables(WaveTables& t, const WaveLds& L, int lane) {
   for (int i = 0; i < kEdgeSlots; ++i) asm volatile("" : "+v"(t.cv[i]));
 #pragma unroll
   for (int k = 0; k < kChkSlots; ++k) asm volatile("" : "+v"(t.pk[k][0]), "+v"(t.pk[k][1]));
+  return padmask;
 }
 
 struct BpArgs {
@@ -497,14 +544,12 @@ __global__ __launch_bounds__(kWave, BP_WAVES_PER_EU) void k_bp(BpArgs a) {
   __shared__ WaveLds L;
   const int lane = threadIdx.x;
   WaveTables tb;
-  load_tables(tb, L, lane);
-  init_poff(L, lane);
+  const uint32_t padmask = load_tables(tb, L, lane);
   for (int n = lane; n < 256; n += kWave) L.bits[n] = 0;
-  for (int e = lane; e < kEdgePad + 8; e += kWave) L.msg[2 * e + 1] = 1.0;
-  __syncthreads();
-  // edge slot 8 holds edges 512..575: lanes >= 10 are padding; their V->C argument is pinned to
-  // 1.0 so the padding keeps every numerator of the division fast path non-zero
-  const bool pad8 = lane + kWave * (kEdgeSlots - 1) >= FT8_LDPC_E;
+  // constant lanes (position 31 of a block) never store a message; padding variables (variable
+  // slot 2, lanes >= 46) never store their V->C arguments
+  const bool st_lane = !const_pos(lane);
+  const bool var2 = lane + kWave * (kVarSlots - 1) < FT8_LDPC_N;
 
   // work counters, per wave; flushed once when the wave retires (same-address atomics per
   // candidate would serialise in L2)
@@ -538,7 +583,12 @@ __global__ __launch_bounds__(kWave, BP_WAVES_PER_EU) void k_bp(BpArgs a) {
     // three tov, forms the hard decision c + ((t0 + t1) + t2) and the three variable->check sums
     // (c + t_a) + t_b, and writes the clipped -T/2 into each edge's slot; (B) parity per check from
     // the decision bytes; (C) edge-major: fast_tanh -> toc; (D) check products -> fast_atanh -> tov.
-    for (int e = lane; e < kEdgePad + 8; e += kWave) L.msg[2 * e] = 0.0;
+    // tov = 0 on every edge; the constants and the padding positions hold 1.0 (the opaque mask
+    // keeps the nine initial values from being hoisted out of the candidate loop and spilled)
+    uint32_t pm = padmask | (const_pos(lane) ? 0x1FFu : 0u);
+    asm volatile("" : "+v"(pm));
+#pragma unroll
+    for (int i = 0; i < kEdgeSlots; ++i) L.msg[lane + kWave * i] = ((pm >> i) & 1u) ? 1.0 : 0.0;
     for (int n = lane; n < kVarPad; n += kWave) L.bits[n] = 0;  // the hard decision if no sweep runs
     __syncthreads();
     int min_errors = FT8_LDPC_M;
@@ -571,9 +621,11 @@ __global__ __launch_bounds__(kWave, BP_WAVES_PER_EU) void k_bp(BpArgs a) {
         const double c0 = c + t0;
         const double T0 = (c + t1) + t2, T1 = c0 + t2, T2 = c0 + t1;
         // fast_tanh's np.clip (no NaN reaches here)
-        *(__attribute__((address_space(3))) double*)(uintptr_t)a0 = __builtin_fmin(__builtin_fmax(-T0 / 2, -4.97), 4.97);
-        *(__attribute__((address_space(3))) double*)(uintptr_t)a1 = __builtin_fmin(__builtin_fmax(-T1 / 2, -4.97), 4.97);
-        *(__attribute__((address_space(3))) double*)(uintptr_t)a2 = __builtin_fmin(__builtin_fmax(-T2 / 2, -4.97), 4.97);
+        if (j < kVarSlots - 1 || var2) {
+          *(__attribute__((address_space(3))) double*)(uintptr_t)a0 = __builtin_fmin(__builtin_fmax(-T0 / 2, -4.97), 4.97);
+          *(__attribute__((address_space(3))) double*)(uintptr_t)a1 = __builtin_fmin(__builtin_fmax(-T1 / 2, -4.97), 4.97);
+          *(__attribute__((address_space(3))) double*)(uintptr_t)a2 = __builtin_fmin(__builtin_fmax(-T2 / 2, -4.97), 4.97);
+        }
       }
       sweep_sync();
       // all-zero hard decision -> stop (ldpc_decoder.py:76-78)
@@ -593,8 +645,7 @@ __global__ __launch_bounds__(kWave, BP_WAVES_PER_EU) void k_bp(BpArgs a) {
       }
       double x[kEdgeSlots];
 #pragma unroll
-      for (int i = 0; i < kEdgeSlots; ++i) x[i] = L.msg[2 * (lane + kWave * i)];
-      x[kEdgeSlots - 1] = pad8 ? 1.0 : x[kEdgeSlots - 1];
+      for (int i = 0; i < kEdgeSlots; ++i) x[i] = L.msg[lane + kWave * i];
       // variable -> check messages: toc = fast_tanh(-Tnm / 2), three interleaved divisions at a time
 #pragma unroll
       for (int g = 0; g < kEdgeSlots; g += kDivGroup) {
@@ -607,8 +658,10 @@ __global__ __launch_bounds__(kWave, BP_WAVES_PER_EU) void k_bp(BpArgs a) {
         }
         div_rn<kDivGroup>(&x[g], na, nb);
       }
+      if (st_lane) {
 #pragma unroll
-      for (int i = 0; i < kEdgeSlots; ++i) L.msg[2 * (lane + kWave * i)] = x[i];
+        for (int i = 0; i < kEdgeSlots; ++i) L.msg[lane + kWave * i] = x[i];
+      }
       sweep_sync();
       // check -> variable messages: tov = -2 fast_atanh(prod of the other toc of the check, in row
       // order, from 1.0).  The six factor addresses are the row address plus the bytes of the
@@ -642,8 +695,10 @@ __global__ __launch_bounds__(kWave, BP_WAVES_PER_EU) void k_bp(BpArgs a) {
         }
         div_rn<kDivGroup, true>(&x[g], na, nb);  // tov = -2 fast_atanh(Tmn)
       }
+      if (st_lane) {
 #pragma unroll
-      for (int i = 0; i < kEdgeSlots; ++i) L.msg[2 * (lane + kWave * i)] = x[i];
+        for (int i = 0; i < kEdgeSlots; ++i) L.msg[lane + kWave * i] = x[i];
+      }
       passes++;
       sweep_sync();
     }
