@@ -16,8 +16,8 @@
 // HBM (coalesced across lanes, window applied on the fly), the epilogue writes the kept bins of the
 // dB waterfall row-contiguously (waterfall layout [slot][frame][bin], frequency fastest).
 //
-// Precision: float32 samples (and int16 WAV samples, scaled x/32767 in float32 as read_wave_file
-// does) are transformed in float32 and produce a float32 waterfall, as SciPy does for complex64;
+// Precision: (this file is compiled with FMA contraction, see the Makefile) float32 samples (and
+// int16 WAV samples, scaled x/32767 in float32 as read_wave_file does) are transformed in float32 and produce a float32 waterfall, as SciPy does for complex64;
 // float64 / complex128 input runs in float64 (SciPy complex128).  The FFT is not bit-identical to
 // pocketfft; tests bound the difference (tests/test_gpu_stft.py).
 #include "ft8_internal.h"
