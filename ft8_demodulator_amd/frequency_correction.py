@@ -82,11 +82,11 @@ def _drift_params(params, fs, sym_bin, sym_t) -> _lib.Ft8DriftParams:
 def detect_signal_continuity(max_freq_indices, window_size=8, max_variance=10.0):
     """frequency_correction.py:42-115 -> (segments [(start, end)], continuity metric), on the GPU
     (ft8_drift_fit stage 1; the PNG of :84-93 is not written)."""
-    torch = _lib.require_gpu()
     idx = np.asarray(max_freq_indices)
     n = len(idx)
-    if n < window_size:
+    if n < window_size:  # :57-58
         return [], np.zeros(n)
+    torch = _lib.require_gpu()
     if idx.size and (idx.min() < 0 or idx.max() >= 8192):
         raise ValueError("argmax indices must lie in [0, 8192)")
     ctx = _lib.context()

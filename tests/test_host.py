@@ -124,3 +124,31 @@ def test_codeword_bits_batch_matches_scalar(oracle):
     for i in range(64):
         assert np.array_equal(got[i], synth.codeword_bits(bytes(pay[i])))
         assert oracle.ldpc_check(got[i]) == 0
+
+
+def test_drift_params_host_logic():
+    """frequency_correction mirror: default filling mutates the caller's dict like the reference
+    (frequency_correction.py:165-171), the C struct carries every field, short inputs return
+    before touching the GPU, and the GPU path fails loudly without one (no CPU fallback)."""
+    import torch
+    from ft8_demodulator_amd import _lib
+    from ft8_demodulator_amd import frequency_correction as FC
+    p = {"steps_per_symbol": 8}
+    out = FC._fill_params(p)
+    assert out is p and p["steps_per_symbol"] == 8 and p["poly_degree"] == 2 and p["window_size_factor"] == 4
+    c = FC._drift_params(p, 12000, 6.25, 0.16)
+    assert (c.sample_rate, c.sym_bin, c.sym_t, c.max_variance_factor) == (12000.0, 6.25, 0.16, 0.0001)
+    assert (c.bins_per_tone, c.steps_per_symbol, c.nsync_sym, c.ndata_sym, c.window_size_factor,
+            c.fit_middle_percent, c.poly_degree, c.precise_sync) == (2, 8, 7, 58, 4, 100, 2, 1)
+    assert ctypes_size(_lib.Ft8DriftParams) == 64 and _lib.DRIFT_RESULT_DTYPE.itemsize == 72
+    segs, m = FC.detect_signal_continuity(np.arange(5), window_size=8)
+    assert segs == [] and m.shape == (5,)
+    if not torch.cuda.is_available():
+        import pytest
+        with pytest.raises(_lib.Ft8Error):
+            FC.correct_frequency_drift(np.zeros(100000, complex), 12000, 6.25, 0.16)
+
+
+def ctypes_size(t):
+    import ctypes
+    return ctypes.sizeof(t)
