@@ -312,6 +312,27 @@ __device__ __forceinline__ bool argmax_better(CT av, int ai, CT bv, int bi) {
   return ai < bi;
 }
 
+template <typename CT>
+__device__ __forceinline__ CT db_of(CT v) {
+  if constexpr (sizeof(CT) == 4) return 10.0f * log10f(v);
+  else return 10.0 * log10(v);
+}
+
+// np.argmax order of the dB values 10 log10(level) decided on the levels: levels further apart
+// than a relative 1e-9 (float64; 1e-4 for float32 -- far above the log's few-ulp error) order their
+// dB values the same way; closer ones (and NaN) compare their dB values exactly, first index on
+// ties.  Every decision equals the comparison of the (dB, -index) keys, so any reduction tree
+// returns np.argmax of the dB row while taking a log only for near ties.
+template <typename CT>
+__device__ __forceinline__ bool level_better(CT la, int ia, CT lb, int ib) {
+  constexpr CT eps = sizeof(CT) == 4 ? (CT)1e-4 : (CT)1e-9;
+  if (la == la && lb == lb) {
+    if (la > lb * ((CT)1 + eps)) return true;
+    if (lb > la * ((CT)1 + eps)) return false;
+  }
+  return argmax_better(db_of(la), ia, db_of(lb), ib);
+}
+
 template <typename InT, bool CPLX, typename CT, int MAXV>
 // two resident waves per SIMD for P <= 4096 (the LDS allows two float64 3840-point workgroups per
 // CU; the radix-16/15 stages then fit 256 VGPRs), one for the 8192-point variant
@@ -364,19 +385,12 @@ __global__ __launch_bounds__(kThreads, (MAXV <= 16 ? 2 : 1)) void k_stft(StftArg
     const CT pw = (X.x * X.x + X.y * X.y) * scale;
     return (CT)1e-12 + pw;
   };
-  auto db_of = [](CT v) -> CT {
-    if constexpr (sizeof(CT) == 4) return 10.0f * log10f(v);
-    else return 10.0 * log10(v);
-  };
   if (a.argmax == nullptr) {
     CT* out = reinterpret_cast<CT*>(a.out) + ((int64_t)slot * a.nt_out + fi) * a.nf_out;
     for (int i = threadIdx.x; i < a.nf_out; i += kThreads) out[i] = db_of(level(i));
     return;
   }
-  // argmax (np.argmax of the dB row).  The log is monotonic, so only bins whose level lies within
-  // rounding of the largest level can hold the largest dB value: pass 1 finds the largest level,
-  // pass 2 takes the log of the bins within a relative 1e-9 (float64; 1e-4 for float32, far above
-  // the log's few-ulp error) of it and compares their dB values exactly (first index on ties).
+  // argmax (np.argmax of the dB row) in one pass on the levels (level_better)
   unsigned char* scratch = smem + (size_t)(P + P / 16 + 1) * sizeof(cplx<CT>);
   CT* sv = reinterpret_cast<CT*>(scratch);
   int* si = reinterpret_cast<int*>(scratch + sizeof(CT) * (kThreads / kWave));
@@ -385,43 +399,20 @@ __global__ __launch_bounds__(kThreads, (MAXV <= 16 ? 2 : 1)) void k_stft(StftArg
   int vi = 0x7fffffff;
   for (int i = threadIdx.x; i < a.nf_out; i += kThreads) {
     const CT v = level(i);
-    if (argmax_better(v, i, vm, vi)) { vm = v; vi = i; }
+    if (level_better(v, i, vm, vi)) { vm = v; vi = i; }
   }
 #pragma unroll
   for (int off = kWave / 2; off > 0; off >>= 1) {
     const CT ov = __shfl_xor(vm, off);
     const int oi = __shfl_xor(vi, off);
-    if (argmax_better(ov, oi, vm, vi)) { vm = ov; vi = oi; }
+    if (level_better(ov, oi, vm, vi)) { vm = ov; vi = oi; }
   }
   if ((threadIdx.x & (kWave - 1)) == 0) { sv[w] = vm; si[w] = vi; }
   __syncthreads();
-#pragma unroll
-  for (int k = 0; k < kThreads / kWave; ++k)
-    if (argmax_better(sv[k], si[k], vm, vi)) { vm = sv[k]; vi = si[k]; }
-  const bool vnan = vm != vm;
-  const CT thr = vm * (sizeof(CT) == 4 ? (CT)(1.0 - 1e-4) : (CT)(1.0 - 1e-9));
-  CT bv = -__builtin_huge_val();
-  int bi = 0x7fffffff;
-  for (int i = threadIdx.x; i < a.nf_out; i += kThreads) {
-    const CT v = level(i);
-    if (vnan ? (v != v) : (v >= thr)) {
-      const CT db = db_of(v);
-      if (argmax_better(db, i, bv, bi)) { bv = db; bi = i; }
-    }
-  }
-#pragma unroll
-  for (int off = kWave / 2; off > 0; off >>= 1) {
-    const CT ov = __shfl_xor(bv, off);
-    const int oi = __shfl_xor(bi, off);
-    if (argmax_better(ov, oi, bv, bi)) { bv = ov; bi = oi; }
-  }
-  __syncthreads();  // every thread has read sv / si of pass 1
-  if ((threadIdx.x & (kWave - 1)) == 0) { sv[w] = bv; si[w] = bi; }
-  __syncthreads();
   if (threadIdx.x == 0) {
     for (int k = 1; k < kThreads / kWave; ++k)
-      if (argmax_better(sv[k], si[k], bv, bi)) { bv = sv[k]; bi = si[k]; }
-    a.argmax[(int64_t)slot * nt + fi] = bi;
+      if (level_better(sv[k], si[k], vm, vi)) { vm = sv[k]; vi = si[k]; }
+    a.argmax[(int64_t)slot * nt + fi] = vi;
   }
 }
 
@@ -720,6 +711,7 @@ __global__ __launch_bounds__(kC38Threads, 2) void k_stftc3840(StftArgs a) {
   cplx<CT>* buf = reinterpret_cast<cplx<CT>*>(smem);
   CT* sv = reinterpret_cast<CT*>(smem + (size_t)(kC38P + kC38P / 16 + 1) * sizeof(cplx<CT>));
   int* si = reinterpret_cast<int*>(sv + kC38Threads / kWave);
+  CT* wl = sv + 16;  // the window, staged once per workgroup (registers are the scarce resource)
   const int t = threadIdx.x;
   const int w_id = t / kWave;
   const int nt = a.nt_out;
@@ -731,6 +723,7 @@ __global__ __launch_bounds__(kC38Threads, 2) void k_stftc3840(StftArgs a) {
   const cplx<CT>* tw = reinterpret_cast<const cplx<CT>*>(a.tw);  // W_3840^m
   const CT* win = reinterpret_cast<const CT*>(a.window);
   const bool s1 = t < 240;
+  for (int n = t; n < 1920; n += kC38Threads) wl[n] = win[n];
   // twiddle seeds: stage 2 W_256^k = W_3840^(15 k) (k = t % 16), stage 3 W_3840^t; their powers are
   // formed by complex recurrence each frame (relative error ~15 ulp, far inside the tolerances)
   cplx<CT> s2 = tw[15 * (t & 15)], s3 = tw[t];
@@ -759,14 +752,11 @@ __global__ __launch_bounds__(kC38Threads, 2) void k_stftc3840(StftArgs a) {
       for (int q = 0; q < M; ++q) nx[q] = load_c<InT, CT>(xs, base + t + 240 * (8 - M + q));
     }
     cplx<CT> v[16];
-    // stage 1: radix 16, Ns = 1 -> buf[16 t + k].  The window is re-read each frame (L1-resident;
-    // the opaque pointer keeps the 8 values from being hoisted into registers for the whole walk)
+    // stage 1: radix 16, Ns = 1 -> buf[16 t + k].  The window comes from LDS each frame.
     if (s1) {
-      const CT* wp = win;
-      asm volatile("" : "+s"(wp));
 #pragma unroll
       for (int r = 0; r < 8; ++r) {
-        const CT wv = wp[t + 240 * r];
+        const CT wv = wl[t + 240 * r];
         v[r] = {wv * raw[r].x, wv * raw[r].y};
       }
       dft16_half_t<CT>(v);
@@ -822,52 +812,26 @@ __global__ __launch_bounds__(kC38Threads, 2) void k_stftc3840(StftArgs a) {
         }
       }
     } else {
-      // two-pass argmax of the dB row (see k_stft): largest level, then exact dB near it
+      // one-pass argmax of the dB row on the levels (level_better)
       CT vm = -__builtin_huge_val();
       int vi = 0x7fffffff;
 #pragma unroll
       for (int r = 0; r < 15; ++r) {
         const int k = t + 256 * r;
-        if (k >= k_lo && k < k_hi && argmax_better(lv[r], k, vm, vi)) { vm = lv[r]; vi = k; }
+        if (k >= k_lo && k < k_hi && level_better(lv[r], k, vm, vi)) { vm = lv[r]; vi = k; }
       }
 #pragma unroll
       for (int off = kWave / 2; off > 0; off >>= 1) {
         const CT ov = __shfl_xor(vm, off);
         const int oi = __shfl_xor(vi, off);
-        if (argmax_better(ov, oi, vm, vi)) { vm = ov; vi = oi; }
+        if (level_better(ov, oi, vm, vi)) { vm = ov; vi = oi; }
       }
       if ((t & (kWave - 1)) == 0) { sv[w_id] = vm; si[w_id] = vi; }
       __syncthreads();
-#pragma unroll
-      for (int k = 0; k < kC38Threads / kWave; ++k)
-        if (argmax_better(sv[k], si[k], vm, vi)) { vm = sv[k]; vi = si[k]; }
-      const bool vnan = vm != vm;
-      const CT thr = vm * (sizeof(CT) == 4 ? (CT)(1.0 - 1e-4) : (CT)(1.0 - 1e-9));
-      CT bv = -__builtin_huge_val();
-      int bi = 0x7fffffff;
-#pragma unroll
-      for (int r = 0; r < 15; ++r) {
-        const int k = t + 256 * r;
-        if (k >= k_lo && k < k_hi && (vnan ? (lv[r] != lv[r]) : (lv[r] >= thr))) {
-          CT db;
-          if constexpr (sizeof(CT) == 4) db = 10.0f * log10f(lv[r]);
-          else db = 10.0 * log10(lv[r]);
-          if (argmax_better(db, k, bv, bi)) { bv = db; bi = k; }
-        }
-      }
-#pragma unroll
-      for (int off = kWave / 2; off > 0; off >>= 1) {
-        const CT ov = __shfl_xor(bv, off);
-        const int oi = __shfl_xor(bi, off);
-        if (argmax_better(ov, oi, bv, bi)) { bv = ov; bi = oi; }
-      }
-      __syncthreads();  // pass-1 values read by every thread
-      if ((t & (kWave - 1)) == 0) { sv[w_id] = bv; si[w_id] = bi; }
-      __syncthreads();
       if (t == 0) {
         for (int k = 1; k < kC38Threads / kWave; ++k)
-          if (argmax_better(sv[k], si[k], bv, bi)) { bv = sv[k]; bi = si[k]; }
-        a.argmax[(int64_t)slot * nt + f] = bi - k_lo;
+          if (level_better(sv[k], si[k], vm, vi)) { vm = sv[k]; vi = si[k]; }
+        a.argmax[(int64_t)slot * nt + f] = vi - k_lo;
       }
     }
     // slide the raw samples by M positions
@@ -885,7 +849,7 @@ hipError_t launch_c3840(const StftLaunch& L, StftArgs a, hipStream_t s) {
   const int chunks = (a.nt_out + kC38Chunk - 1) / kC38Chunk;
   a.per_xcd = (int)(((int64_t)chunks * L.n_slots + 7) / 8);
   const dim3 grid((unsigned)(8 * a.per_xcd));
-  const size_t lds = (size_t)(kC38P + kC38P / 16 + 1) * sizeof(cplx<CT>) + 64;
+  const size_t lds = (size_t)(kC38P + kC38P / 16 + 1) * sizeof(cplx<CT>) + 16 * sizeof(CT) + 1920 * sizeof(CT);
   auto go = [&](auto kern) {
     if (lds > 64 * 1024) {
       hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
