@@ -104,8 +104,10 @@ class StreamDecoder:
         cap = self.dec.cap
         recs = self.hout[i][: nb * cap * _lib.RESULT_DTYPE.itemsize].numpy().view(_lib.RESULT_DTYPE).reshape(nb, cap)
         cnt = self.hcnt[i][:nb].numpy()
-        return [records_to_results(recs[s, : min(int(cnt[s]), cap)].copy(), self.fs, self.bpt, False)
-                for s in range(nb)]
+        out = [[] for _ in range(nb)]
+        for s in np.flatnonzero(cnt > 0):  # most slots decode nothing: skip them without a copy
+            out[s] = records_to_results(recs[s, : min(int(cnt[s]), cap)].copy(), self.fs, self.bpt, False)
+        return out
 
     def decode_batches(self, batches: Iterable) -> Iterator[List[list]]:
         """Yield per-slot results of each batch, in order; batch k+1 uploads while batch k decodes."""
