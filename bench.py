@@ -403,6 +403,10 @@ def main():
     stft_bytes = S * (x.shape[1] * 4 + plan.T * plan.F * 4)
     stft_gbs = stft_bytes / (stft_ms * 1e-3) / 1e9
     cand_per_s = cn["candidates"] / K * world / (elapsed / K)
+    # BASELINE.md's whole-step figure: B_slot = N s_in + 2 F T 4 + K (58 8 4 + 174 8 2 + 40)
+    # algorithmic bytes per slot; slots/s x B_slot vs the 8 TB/s HBM peak
+    b_slot = x.shape[1] * 4 + 2 * plan.F * plan.T * 4 + kw["max_candidates"] * (58 * 8 * 4 + 174 * 8 * 2 + 40)
+    step_gbs = value / world * b_slot / 1e9
 
     stress = None
     if world == 1 and not args.no_bp_stress:
@@ -457,6 +461,10 @@ def main():
                      "frac": ach_tf / FP64_VECTOR_PEAK_TFLOPS, "traffic": hbm("ft8::k_bp"),
                      "flops_per_launch": flops, "launch_ms": bp_ms,
                      "bp_passes_per_launch": cn["passes"] / K, "candidates_per_launch": cn["candidates"] / K},
+        "step_hbm": {"what": "BASELINE.md whole-step accounting: slots/s per GPU x B_slot algorithmic bytes "
+                             "(the step is FP64-VALU bound in k_bp, so this fraction is low by construction)",
+                     "bytes_per_slot": b_slot, "achieved": step_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": step_gbs / HBM_PEAK_GBS},
         "roofline_hbm": {"kernel": "k_stft", "bound": "hbm", "achieved": stft_gbs, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": stft_gbs / HBM_PEAK_GBS, "traffic": hbm("ft8::k_stft"),
                          "bytes_per_launch": stft_bytes, "launch_ms": stft_ms},
