@@ -168,6 +168,7 @@ def subtract_redecode(dev, n_slots=334, signals=50, iters=50, reps=3):
                     "has no second pass"}
 
 
+GATHER_PER_SLOT = 8  # compacted all-gather rows per slot at N > 1 (distributed.gather_decodes)
 DRIFT_PARAMS = {"bins_per_tone": 2, "steps_per_symbol": 8}  # the reference test's correction params
 
 
@@ -342,7 +343,7 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     from ft8_demodulator_amd import SlotDecoder, synth
-    from ft8_demodulator_amd.distributed import gather_records
+    from ft8_demodulator_amd.distributed import gather_decodes
 
     S = args.slots
     x, _ = synth.make_slots(S, args.signals, fs=12000, snr_db=(-24.0, -10.0), seed=100000 * (rank + 1),
@@ -351,10 +352,14 @@ def main():
     dec = SlotDecoder(12000, 2, 2, device=dev, **kw)
     ctx = dec.ctx
 
+    # N > 1: every step all-gathers the decodes, compacted on the device into GATHER_PER_SLOT x S
+    # rows per rank (≈1 decode per slot here); a rank whose total exceeds that is reported below
+    gathered = []
+
     def step():
         out, counts = dec.run(x)
         if world > 1:
-            gather_records(out, counts)
+            gathered[:] = [gather_decodes(out, counts, dec.cap, GATHER_PER_SLOT * S)[2]]
         return counts
 
     for _ in range(args.warmup):
@@ -459,7 +464,9 @@ def main():
                                "K=300 candidates, min_score=2, 20 BP iterations (config 5 shape at N>1)",
                    "slots_per_gpu": S, "sample_rate": 12000, "samples_per_slot": int(x.shape[1]),
                    "max_candidates": 300, "min_score": 2, "max_iterations": 20,
-                   "parallelism": f"slot-sharded x{world}, RCCL all-gather of result records"},
+                   "parallelism": f"slot-sharded x{world}" + (
+                       f", one RCCL all-gather per step of the decodes compacted on the device "
+                       f"({GATHER_PER_SLOT} rows/slot/rank)" if world > 1 else "")},
         "ldpc_candidates_per_s": cand_per_s,
         "decodes_per_step": decoded,  # successful decodes in one step's batch (every step decodes the same batch)
         "roofline": {"kernel": "k_bp (float64 BP + CRC)", "bound": "fp64-valu",
@@ -481,6 +488,12 @@ def main():
         "drift_correct": drift,
         "cpu_baseline": cpu,
     }
+    if world > 1:
+        totals = gathered[0].cpu().tolist()
+        line["gather"] = {"rows_per_rank": GATHER_PER_SLOT * S,
+                          "bytes_per_rank": GATHER_PER_SLOT * S * 40 + 4 * S + 8,
+                          "decodes_per_rank_last_step": totals,
+                          "truncated": any(t > GATHER_PER_SLOT * S for t in totals)}
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

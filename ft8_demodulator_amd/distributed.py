@@ -1,5 +1,6 @@
 """Multi-GPU sharding of slot batches: one process per GPU, slots split by contiguous ranges, one
-all-gather of the fixed-size result records (ft8_result, 40 B) per batch.
+all-gather of the result records (ft8_result, 40 B) per batch -- either the fixed per-slot buffers
+(gather_records) or, far smaller, the decodes compacted on the device (gather_decodes).
 
 Slots are independent: no data-path collective is needed to decode.  The only
 exchange is gathering every rank's decodes, e.g. to rank 0 for reporting; over RCCL ("nccl" backend)
@@ -27,3 +28,51 @@ def gather_records(records, counts, group=None):
     dist.all_gather_into_tensor(rec_all, records.contiguous().view(-1), group=group)
     dist.all_gather_into_tensor(cnt_all, counts.contiguous().view(-1), group=group)
     return rec_all.view((world,) + tuple(records.shape)), cnt_all.view((world,) + tuple(counts.shape))
+
+
+REC_BYTES = 40  # sizeof(ft8_result)
+
+
+def compact_records(records, counts, cap, capacity):
+    """Pack the per-slot record buffer (uint8 [S*cap*40], slot s's decodes in rows [s*cap, s*cap +
+    counts[s])) into `capacity` dense rows in slot order, on the records' device and without a host
+    sync.  Returns (dense uint8 [capacity, 40], total int64 0-d tensor = sum of min(counts, cap));
+    total > capacity means rows beyond `capacity` were dropped (every record keeps its own `slot`)."""
+    import torch
+    dev = records.device
+    S = counts.numel()
+    c = counts.to(torch.int64).clamp(0, cap)
+    off = torch.cumsum(c, 0) - c
+    j = torch.arange(cap, device=dev, dtype=torch.int64)
+    dest = off[:, None] + j[None, :]
+    keep = (j[None, :] < c[:, None]) & (dest < capacity)
+    dest = torch.where(keep, dest, torch.full_like(dest, capacity))  # row `capacity` is a dump row
+    dense = torch.zeros((capacity + 1, REC_BYTES), dtype=torch.uint8, device=dev)
+    dense.index_copy_(0, dest.view(-1), records[: S * cap * REC_BYTES].view(S * cap, REC_BYTES))
+    return dense[:capacity], c.sum()
+
+
+def gather_decodes(records, counts, cap, capacity, group=None):
+    """One all-gather of every rank's decodes, compacted: each rank packs its records into
+    `capacity` dense rows (compact_records) plus its per-slot counts and total into one byte buffer,
+    so the exchange moves capacity*40 + 4*S + 8 bytes per rank instead of S*cap*40.
+
+    Returns (records uint8 [world, capacity, 40], counts int32 [world, S], totals int64 [world]) on
+    every rank; rank r's first min(totals[r], capacity) rows are its decodes in slot order, and
+    totals[r] > capacity flags a truncated rank (raise `capacity`)."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    S = counts.numel()
+    dense, total = compact_records(records, counts, cap, capacity)
+    nrec = capacity * REC_BYTES
+    buf = torch.empty(nrec + 4 * S + 8, dtype=torch.uint8, device=records.device)
+    buf[:nrec] = dense.reshape(-1)
+    buf[nrec:nrec + 4 * S] = counts.to(torch.int32).contiguous().view(torch.uint8)
+    buf[nrec + 4 * S:] = total.reshape(1).view(torch.uint8)
+    out = torch.empty(world * buf.numel(), dtype=torch.uint8, device=records.device).view(world, -1)
+    dist.all_gather_into_tensor(out.view(-1), buf, group=group)
+    recs = out[:, :nrec].reshape(world, capacity, REC_BYTES)
+    cnts = out[:, nrec:nrec + 4 * S].contiguous().view(torch.int32)
+    totals = out[:, nrec + 4 * S:].contiguous().view(torch.int64).reshape(world)
+    return recs, cnts, totals

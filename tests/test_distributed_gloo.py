@@ -20,9 +20,13 @@ def _worker(rank, world, port, n_slots, q):
         rec.view(hi - lo, cap, 40)[:, :, 0] = torch.arange(lo, hi, dtype=torch.uint8)[:, None]
         cnt = torch.arange(lo, hi, dtype=torch.int32) % 4
         r_all, c_all = gather_records(rec, cnt)
-        q.put((rank, lo, hi, r_all.view(world, hi - lo, cap, 40)[:, :, 0, 0].tolist(), c_all.tolist()))
+        from ft8_demodulator_amd.distributed import gather_decodes
+        d_all, dc_all, tot = gather_decodes(rec, cnt, cap, 4)
+        compact = [d_all[r, :min(int(tot[r]), 4), 0].tolist() for r in range(world)]
+        q.put((rank, lo, hi, r_all.view(world, hi - lo, cap, 40)[:, :, 0, 0].tolist(), c_all.tolist(),
+               compact, dc_all.tolist(), tot.tolist()))
       except Exception as e:  # noqa: BLE001
-        q.put((rank, "error", repr(e), None, None))
+        q.put((rank, "error", repr(e), None, None, None, None, None))
         raise
     finally:
         dist.destroy_process_group()
@@ -50,6 +54,11 @@ def test_gloo_world2_gather():
     for p in ps:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for rank, lo, hi, recs, cnts in out:
+    for rank, lo, hi, recs, cnts, compact, dcnts, tot in out:
         assert recs == [[0, 1, 2, 3], [4, 5, 6, 7]]
         assert cnts == [[0, 1, 2, 3], [0, 1, 2, 3]]
+        # compacted: slot s contributes min(count, cap) rows tagged s, in slot order; rank 1 holds
+        # 0 + 1 + 2 + 3 = 6 decodes for a capacity of 4, so its total flags the truncation
+        assert dcnts == cnts
+        assert tot == [0 + 1 + 2 + 3, 0 + 1 + 2 + 3]
+        assert compact == [[1, 2, 2, 3], [5, 6, 6, 7]]

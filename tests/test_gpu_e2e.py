@@ -185,3 +185,26 @@ def test_decode_batch_orders_equal_scores_like_the_reference(gpu, oracle):
             assert np.float32(r["score"]) == sc[c], (s, c)
             checked += 1
     assert checked > 0
+
+
+@pytest.mark.gpu
+def test_compacted_records_on_device(gpu):
+    """distributed.compact_records (the N > 1 gather's packing) on real decode output: the dense rows
+    are every slot's decodes in slot order, identical to SlotDecoder.records()."""
+    import numpy as np
+    import torch
+    from ft8_demodulator_amd import SlotDecoder, _lib, synth
+    from ft8_demodulator_amd.distributed import compact_records
+    x, _ = synth.make_slots(12, 30, seed=321, device="cuda")
+    dec = SlotDecoder(12000, 2, 2, 300, 2, 20)
+    out, counts = dec.run(x)
+    dense, total = compact_records(out, counts, dec.cap, 64)
+    torch.cuda.synchronize()
+    per_slot = dec.records(x)
+    want = np.concatenate([r for r in per_slot]) if per_slot else np.zeros(0, _lib.RESULT_DTYPE)
+    assert int(total) == len(want) >= 3
+    got = dense[: int(total)].cpu().numpy().reshape(-1).view(_lib.RESULT_DTYPE)
+    assert got.tobytes() == want.tobytes()
+    small, total2 = compact_records(out, counts, dec.cap, 3)
+    assert int(total2) == len(want) and small.shape[0] == 3
+    assert small.cpu().numpy().reshape(-1).view(_lib.RESULT_DTYPE).tobytes() == want[:3].tobytes()
