@@ -155,17 +155,23 @@ def test_decode_batch_orders_equal_scores_like_the_reference(gpu, oracle):
     """ft8_decode_batch leaves equal scores in scan order through LLR/BP (warn bit 3), replays the
     reference heap in k_llr's first workgroups and lets k_compact apply the order: every record's
     cand_index, time, frequency and score follow the oracle's heapq order of the same score grid,
-    and the tie flag (bit 0) matches.  The bench workload has such slots."""
+    and the tie flag (bit 0) matches.  Such slots are rare (about 1 in 100 of the bench workload's,
+    depending on the waterfall's last bits), so batches of the bench workload are drawn until one
+    holds them."""
     import torch
     from ft8_demodulator_amd import FT8Waterfall, SlotDecoder, _device, _lib, synth
     from ft8_demodulator_amd._pipeline import make_plan
-    x, _ = synth.make_slots(256, 50, seed=100000, device="cuda")
     dec = SlotDecoder(12000, 2, 2, 300, 2, 20)
-    recs = dec.records(x)
-    w = torch.zeros(256, dtype=torch.int32, device="cuda")
-    dec.ctx.check(_lib.lib().ft8_select_warnings(dec.ctx.handle, _lib.ptr(w), 256, _lib.stream_handle()), "warn")
-    w = w.cpu().numpy()
-    slots = np.nonzero(w & 8)[0]
+    for seed in (100000, 200000, 300000, 400000, 500000, 600000):
+        x, _ = synth.make_slots(256, 50, seed=seed, device="cuda")
+        recs = dec.records(x)
+        w = torch.zeros(256, dtype=torch.int32, device="cuda")
+        dec.ctx.check(_lib.lib().ft8_select_warnings(dec.ctx.handle, _lib.ptr(w), 256, _lib.stream_handle()),
+                      "warn")
+        w = w.cpu().numpy()
+        slots = np.nonzero(w & 8)[0]
+        if len(slots):
+            break
     assert len(slots) >= 1 and np.all(w[slots] & 4)
     plan = make_plan(x.shape[1], 12000, 2, 2)
     checked = 0
