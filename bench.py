@@ -9,6 +9,12 @@ step ends with an RCCL all-gather of every rank's result records (the path's one
     python bench.py [--gpus N] [--steps K] [--warmup W] [--slots S] [--no-cpu]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
+`python bench.py --gpus N` with N > 1 and no WORLD_SIZE in the environment launches the N ranks
+itself (a torch.distributed.run child, before this process touches the GPU) and exits with its
+code; it exits non-zero when fewer than N GPUs are visible or when WORLD_SIZE disagrees with --gpus.
+Rank r decodes global slots [256 r, 256 (r + 1)) (per-slot seeds 100000 + slot), so the N = 1 batch
+is the first shard of every larger run.
+
 Prints ONE JSON line on rank 0.  Besides the contract fields it carries:
   roofline      the dominant kernel (k_bp: LLR + float64 BP + CRC), FLOP-rate vs the FP64 vector peak
   roofline_hbm  the HBM-bound STFT kernel, GB/s vs the 8 TB/s HBM peak
@@ -20,7 +26,10 @@ Prints ONE JSON line on rank 0.  Besides the contract fields it carries:
                 complex128 beacon signals (12 kHz, 3 x 12.64 s, steps_per_symbol 8): signals/s, the
                 dominant kernel's roofline and the oracle port's CPU rate (N=1)
   h2d_stream    the same slots as int16 PCM in pinned host memory, upload overlapped with decode (N=1)
-  cpu_baseline  the oracle port (oracle/, C + scipy) on a bounded sample of the same slots (rank 0, N=1)
+  cpu_baseline  the oracle port (oracle/, C + scipy) on the first slots of rank 0's own batch -- the
+                same bytes the GPU decodes (rank 0, N=1)
+  parity        those slots' GPU decodes vs the oracle's: payload + CRC multisets, ordered lists
+  reference_measured  the reference's own single-thread figure, for context
 """
 import argparse
 import json
@@ -49,37 +58,95 @@ def bp_flops_per_pass():
     return f
 
 
+def host_cores():
+    """Worker processes for the CPU legs: the host cores this process may use -- sched_getaffinity,
+    bounded by the cgroup CPU quota and by OMP_NUM_THREADS when set (the GPU box sets it to this
+    job's CPU share; affinity there lists the whole machine).  -> (cores, basis string)."""
+    aff = len(os.sched_getaffinity(0))
+    n, basis = aff, [f"sched_getaffinity={aff}"]
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+            n = min(n, max(1, int(quota)))
+            basis.append(f"cgroup cpu.max={quota:g}")
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+        basis.append(f"OMP_NUM_THREADS={omp}")
+    return max(1, n), "min(" + ", ".join(basis) + ")"
+
+
+def _worker_init():
+    import torch
+    torch.set_num_threads(1)
+
+
+def cpu_synth_worker(args):
+    """One slot of the benchmark workload synthesised on the CPU (synth.make_slots, per-slot seed)."""
+    from ft8_demodulator_amd import synth
+    seed, signals = args
+    x, _ = synth.make_slots(1, signals, fs=12000, snr_db=(-24.0, -10.0), seeds=[seed], device="cpu")
+    return x[0].numpy()
+
+
 def cpu_worker(args):
-    import numpy as np  # noqa: F401
     from oracle import oracle as O
     x, kw = args
-    return len(O.decode_ft8_message(x, 12000, **kw))
+    return [(bytes(r[0]).hex(), int(r[1]), float(r[5]), float(r[6]), float(r[7]))
+            for r in O.decode_ft8_message(x, 12000, **kw)]
 
 
-def cpu_baseline(kw, n_slots, procs, seed, signals):
-    """Oracle port on `n_slots` slots of the benchmark workload, `procs` worker processes.
-
-    Runs before this process touches the GPU, so the workers inherit no device state.  The slots
-    use the same per-slot seeds (payloads, frequencies, start times, SNRs) as the first slots of
-    rank 0's GPU batch; their noise comes from the CPU generator, so the samples are the same
-    workload, not the same bytes."""
+def cpu_baseline(kw, n_slots, procs, basis, seed0, signals):
+    """Oracle port (oracle/, C + scipy) on the first n_slots slots of rank 0's batch, `procs` worker
+    processes.  The slots are synthesised here on the CPU and then uploaded as the first n_slots
+    rows of the GPU batch, so the CPU and the GPU decode the SAME bytes (the decodes are compared
+    in the `parity` object).  Runs before this process touches the GPU, so the forked workers
+    inherit no device state.  -> (baseline dict, [n_slots, N] float32 samples, per-slot decodes)."""
     import multiprocessing as mp
-    from ft8_demodulator_amd import synth
+    import numpy as np
     from oracle import oracle as O
     O.lib()
-    x, _ = synth.make_slots(n_slots, signals, fs=12000, snr_db=(-24.0, -10.0), seed=seed, device="cpu")
-    xs = [x[i].numpy() for i in range(n_slots)]
     ctx = mp.get_context("fork")
-    with ctx.Pool(procs) as pool:
+    with ctx.Pool(procs, initializer=_worker_init) as pool:
+        t0 = time.perf_counter()
+        xs = pool.map(cpu_synth_worker, [(seed0 + b, signals) for b in range(n_slots)], chunksize=1)
+        t_syn = time.perf_counter() - t0
         pool.map(cpu_worker, [(xs[0], kw)] * procs)  # warm the workers (imports, scipy plans)
         t0 = time.perf_counter()
-        pool.map(cpu_worker, [(x, kw) for x in xs], chunksize=1)
+        decodes = pool.map(cpu_worker, [(x, kw) for x in xs], chunksize=1)
         dt = time.perf_counter() - t0
-    return {"value": n_slots / dt, "unit": "slots/s", "cores": procs, "kind": "port",
-            "sample": f"{n_slots} slots of the benchmark workload (same per-slot seeds, K=300, min_score=2, "
-                      f"20 iters); "
-                      f"oracle/ft8_oracle.c + scipy STFT, {procs} processes, {dt:.2f} s wall",
-            "wall_s": dt}
+    base = {"value": n_slots / dt, "unit": "slots/s", "cores": procs, "cores_basis": basis, "kind": "port",
+            "sample": f"the first {n_slots} slots of rank 0's GPU batch (the same float32 bytes; K=300, min_score=2, "
+                      f"20 iters); oracle/ft8_oracle.c + scipy STFT, {procs} processes, {dt:.2f} s wall",
+            "wall_s": dt, "synth_wall_s": t_syn}
+    return base, np.stack(xs), decodes
+
+
+def parity_check(gpu_recs, cpu_decodes, bpt=2):
+    """GPU records (SlotDecoder.records) vs the oracle's decodes of the same slots: payload + CRC
+    multisets per slot (the contract), ordered (payload, crc, time, freq) lists, score deltas."""
+    mism, ordered, dmax, ng, nc = [], 0, 0.0, 0, 0
+    for s, (g, c) in enumerate(zip(gpu_recs, cpu_decodes)):
+        gl = [(bytes(r["payload"]).hex(), int(r["crc_calculated"]), int(r["abs_time"]) / 12000,
+               (int(r["abs_freq"]) / bpt) * 6.25, float(r["score"])) for r in g]
+        ng, nc = ng + len(gl), nc + len(c)
+        if sorted(x[:2] for x in gl) != sorted(x[:2] for x in c):
+            mism.append(s)
+        if [x[:4] for x in gl] == [x[:4] for x in c]:
+            ordered += 1
+            for a, b in zip(gl, c):
+                dmax = max(dmax, abs(a[4] - b[4]))
+    return {"slots": len(cpu_decodes), "decodes_gpu": ng, "decodes_cpu": nc,
+            "payload_crc_multiset_equal": not mism, "mismatching_slots": mism,
+            "ordered_lists_equal_slots": ordered, "max_abs_score_diff": dmax,
+            "note": "CPU = oracle port with scipy's pocketfft STFT; GPU = this build's STFT (dB within "
+                    "1e-3 on strong bins, SURVEY 8(a)): a candidate whose score lies within that error of "
+                    "min_score or of a selection boundary can enter or leave the list; "
+                    "tests/test_gpu_bench_parity.py checks every slot of this batch stage by stage"}
 
 
 def bp_stress(ctx, dev, n=100000, iters=50, reps=3, sigma=0.85):
@@ -98,25 +165,23 @@ def bp_stress(ctx, dev, n=100000, iters=50, reps=3, sigma=0.85):
     def run():
         ctx.check(L.ft8_bp(ctx.handle, _lib.ptr(x), n, iters, None, _lib.ptr(res), st), "ft8_bp")
 
+    ctx.set_timing(True)   # allocates the BP work counters (events are not used below)
+    ctx.set_timing(False)
     run()
     torch.cuda.synchronize()
-    ctx.set_timing(True)
-    ctx.timing(reset=True)
     ctx.counters(reset=True)
     t0 = time.perf_counter()
     for _ in range(reps):
         run()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    ctx.set_timing(False)
-    tm = ctx.timing(reset=True)
     cn = ctx.counters(reset=True)
-    bp_ms = tm["bp"][0] / max(tm["bp"][1], 1)
+    bp_ms = dt / reps * 1e3  # one k_bp launch (+ its 4-byte counter reset) per call, back to back
     flops = (cn["passes"] * bp_flops_per_pass() + cn["iterations"] * 174 * 3) / reps
     tf = flops / (bp_ms * 1e-3) / 1e12
     return {"workload": f"BASELINE config 4 first pass: {n} LLR vectors (codewords of random payloads, "
                         f"(2b-1)+{sigma}*N(0,1), normalised), {iters} BP iterations",
-            "candidates_per_s": n * reps / dt, "ms_per_launch": bp_ms,
+            "candidates_per_s": n * reps / dt, "ms_per_launch": bp_ms, "timing": "wall clock over back-to-back launches",
             "converged_frac": cn["converged"] / max(cn["candidates"], 1),
             "sweeps_per_launch": cn["passes"] / reps,
             "roofline": {"kernel": "k_bp", "bound": "fp64-valu", "achieved": tf, "peak": FP64_VECTOR_PEAK_TFLOPS,
@@ -168,7 +233,6 @@ def subtract_redecode(dev, n_slots=334, signals=50, iters=50, reps=3):
                     "has no second pass"}
 
 
-GATHER_PER_SLOT = 8  # compacted all-gather rows per slot at N > 1 (distributed.gather_decodes)
 DRIFT_PARAMS = {"bins_per_tone": 2, "steps_per_symbol": 8}  # the reference test's correction params
 
 
@@ -308,6 +372,44 @@ def h2d_stream(x, steps, kw):
             "h2d_bytes_per_batch": int(pcm.numel() * 2)}
 
 
+REFERENCE_MEASURED = {
+    "value": 1.0 / 30.5, "unit": "slots/s", "cores": 1,
+    "what": "the reference's own decode_ft8_message (Python/NumPy/SciPy) on one config-2-like slot (50 signals, "
+            "K=300, min_score=2): 30.5 s per slot single-threaded, measured in the survey container (8-core "
+            "Xeon VM, numpy 2.2.6, scipy 1.15.3; SURVEY.md section 6, BASELINE.md section 2) -- not a same-node run"}
+
+STAGE_ORDER = ("stft", "score", "select", "llr", "bp", "compact")
+
+
+def launch_ranks(args):
+    """--gpus N > 1 without a launcher: start N ranks under torch.distributed.run as a child
+    process (this process never touches the GPU) and return its exit code."""
+    import socket
+    import subprocess
+    import torch
+    n_dev = torch.cuda.device_count()  # does not initialise HIP on this image
+    if n_dev < args.gpus:
+        print(f"bench.py: --gpus {args.gpus} requested but only {n_dev} GPU(s) are visible", file=sys.stderr)
+        return 2
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    return subprocess.call(cmd, env=env)
+
+
+def replay_ms(ctx, stage, reps, torch):
+    """Wall-clock duration of one launch of `stage` of the last ft8_decode_batch: `reps`
+    back-to-back re-launches (ft8_replay_stage) between two synchronisations, no events."""
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ctx.replay(stage, reps)
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / reps * 1e3
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -317,23 +419,39 @@ def main():
     ap.add_argument("--signals", type=int, default=50)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-slots", type=int, default=256)
+    ap.add_argument("--replays", type=int, default=10, help="back-to-back launches per stage timing")
     ap.add_argument("--no-bp-stress", action="store_true", help="skip the config-4 BP stress leg")
     ap.add_argument("--no-h2d", action="store_true", help="skip the PCIe-inclusive streaming leg")
     ap.add_argument("--no-subtract", action="store_true", help="skip the config-4 subtract-and-redecode leg")
     ap.add_argument("--no-drift", action="store_true", help="skip the frequency-drift correction leg")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" in os.environ:
+        world = int(os.environ["WORLD_SIZE"])
+        if world != args.gpus:
+            print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
+            sys.exit(2)
+    elif args.gpus > 1:
+        sys.exit(launch_ranks(args))
+    else:
+        world = 1
+    if args.gpus < 1:
+        sys.exit(2)
+
+    import numpy as np
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     kw = dict(max_candidates=300, min_score=2, max_iterations=20)
+    S = args.slots
+    seed0 = 100000 + rank * S  # global slot g uses seed 100000 + g
     cpu = drift_cpu_port = None
+    cpu_x = cpu_dec = None
     if rank == 0 and world == 1 and not args.no_cpu and args.cpu_slots > 0:
-        procs = max(1, min(16, len(os.sched_getaffinity(0))))
-        cpu = cpu_baseline(kw, min(args.cpu_slots, args.slots), procs, 100000, args.signals)
+        procs, basis = host_cores()
+        cpu, cpu_x, cpu_dec = cpu_baseline(kw, min(args.cpu_slots, S), procs, basis, seed0, args.signals)
         if not args.no_drift:
             drift_cpu_port = drift_cpu_baseline(procs)
     torch.cuda.set_device(local)
@@ -342,24 +460,35 @@ def main():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", device_id=dev)
 
-    from ft8_demodulator_amd import SlotDecoder, synth
+    from ft8_demodulator_amd import SlotDecoder, synth, _lib
     from ft8_demodulator_amd.distributed import gather_decodes
 
-    S = args.slots
-    x, _ = synth.make_slots(S, args.signals, fs=12000, snr_db=(-24.0, -10.0), seed=100000 * (rank + 1),
-                            device=dev)
+    # the batch: slots synthesised on the CPU for the CPU leg are uploaded as-is (same bytes), the
+    # rest synthesised on the GPU with the same per-slot seeds
+    n_cpu = 0 if cpu_x is None else cpu_x.shape[0]
+    parts = []
+    if n_cpu:
+        parts.append(torch.from_numpy(cpu_x).to(dev))
+    if S > n_cpu:
+        xg, _ = synth.make_slots(S - n_cpu, args.signals, fs=12000, snr_db=(-24.0, -10.0),
+                                 seeds=[seed0 + b for b in range(n_cpu, S)], device=dev)
+        parts.append(xg)
+    x = torch.cat(parts) if len(parts) > 1 else parts[0]
+    del parts
     torch.cuda.synchronize()
     dec = SlotDecoder(12000, 2, 2, device=dev, **kw)
     ctx = dec.ctx
+    ctx.set_timing(True)   # allocates the device BP work counters; no events are recorded below
+    ctx.set_timing(False)
 
-    # N > 1: every step all-gathers the decodes, compacted on the device into GATHER_PER_SLOT x S
-    # rows per rank (≈1 decode per slot here); a rank whose total exceeds that is reported below
+    # N > 1: every step ends with the data-sized all-gather of the decodes (totals, then exactly
+    # max(total) rows per rank), records carrying global slot ids
     gathered = []
 
     def step():
         out, counts = dec.run(x)
         if world > 1:
-            gathered[:] = [gather_decodes(out, counts, dec.cap, GATHER_PER_SLOT * S)[2]]
+            gathered[:] = [gather_decodes(out, counts, dec.cap, slot_offset=rank * S)]
         return counts
 
     for _ in range(args.warmup):
@@ -376,18 +505,17 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     decoded = int(counts.sum().item())
-    # per-stage device times and BP work counters from a separate pass of the same step (HIP events
-    # between the stages cost ~2 % of the step, so the timed loop above runs without them)
-    KT = max(1, min(args.steps, 10))
-    ctx.set_timing(True)
-    ctx.timing(reset=True)
-    ctx.counters(reset=True)
-    for _ in range(KT):
-        step()
-    torch.cuda.synchronize()
-    ctx.set_timing(False)
-    tm = ctx.timing(reset=True)
-    cn = ctx.counters(reset=True)
+
+    # per-kernel durations: each kernel of the last step re-launched back to back (wall clock, no
+    # events); the BP work counters of those k_bp re-launches give its algorithmic FLOPs
+    R = max(1, args.replays)
+    stage_ms = {}
+    for st in STAGE_ORDER:
+        if st == "bp":
+            ctx.counters(reset=True)
+        stage_ms[st] = replay_ms(ctx, st, R, torch)
+        if st == "bp":
+            cn = ctx.counters(reset=True)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -396,24 +524,26 @@ def main():
         dist.all_reduce(d)
         decoded = int(d.item())
 
+    parity = None
+    if cpu_dec is not None:
+        parity = parity_check(dec.records(x[:n_cpu]), cpu_dec)
+
     total_slots = S * world * args.steps
     value = total_slots / elapsed
     K = args.steps
-    # per-kernel device time (this rank), per step
-    stage_ms = {k: (v[0] / max(v[1], 1)) for k, v in tm.items() if v[1] > 0}
-    bp_ms = stage_ms.get("bp", float("nan"))
-    stft_ms = stage_ms.get("stft", float("nan"))
+    bp_ms = stage_ms["bp"]
+    stft_ms = stage_ms["stft"]
     # dominant kernel: k_bp.  Algorithmic FLOPs per launch from the device counters.
     f_pass = bp_flops_per_pass()
     f_hd = 174 * 3
-    flops = (cn["passes"] * f_pass + cn["iterations"] * f_hd) / KT
+    flops = (cn["passes"] * f_pass + cn["iterations"] * f_hd) / R
     ach_tf = flops / (bp_ms * 1e-3) / 1e12
     # STFT: samples read once (f32) + dB waterfall written once
     from ft8_demodulator_amd._pipeline import make_plan
     plan = make_plan(x.shape[1], 12000)
     stft_bytes = S * (x.shape[1] * 4 + plan.T * plan.F * 4)
     stft_gbs = stft_bytes / (stft_ms * 1e-3) / 1e9
-    cand_per_s = cn["candidates"] / KT * world / (elapsed / K)
+    cand_per_s = cn["candidates"] / R * world / (elapsed / K)
     # BASELINE.md's whole-step figure: B_slot = N s_in + 2 F T 4 + K (58 8 4 + 174 8 2 + 40)
     # algorithmic bytes per slot; slots/s x B_slot vs the 8 TB/s HBM peak
     b_slot = x.shape[1] * 4 + 2 * plan.F * plan.T * 4 + kw["max_candidates"] * (58 * 8 * 4 + 174 * 8 * 2 + 40)
@@ -435,10 +565,13 @@ def main():
 
     # HBM bytes per launch from the committed rocprofv3 PMC summary (tools/pmc_traffic.py; FETCH_SIZE
     # and WRITE_SIZE passes of the same 256-slot workload), or null when it is absent
-    traffic = {}
-    tpath = os.path.join(ROOT, "profiles", "r1_pmc_traffic.json")
-    if os.path.exists(tpath):
-        with open(tpath) as f:
+    import glob
+    traffic, tsrc = {}, None
+    tfiles = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")),
+                    key=lambda p_: int(os.path.basename(p_)[1:].split("_")[0]))
+    if tfiles:
+        tsrc = os.path.relpath(tfiles[-1], ROOT)
+        with open(tfiles[-1]) as f:
             traffic = json.load(f).get("kernels", {})
 
     def hbm(kernel_prefix):
@@ -459,41 +592,46 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32 (STFT, sync score) / f64 (LLR, BP)",
-        "data": "synthetic (ft8_demodulator_amd.synth: 50 GFSK signals/slot, SNR U(-24,-10) dB, unit noise)",
+        "data": "synthetic (ft8_demodulator_amd.synth: 50 GFSK signals/slot, SNR U(-24,-10) dB, unit noise; "
+                "per-slot seeds 100000 + global slot)",
         "config": {"workload": "BASELINE config 3: batch of 256 independent 15-s slots per GPU, 12 kHz, "
                                "K=300 candidates, min_score=2, 20 BP iterations (config 5 shape at N>1)",
                    "slots_per_gpu": S, "sample_rate": 12000, "samples_per_slot": int(x.shape[1]),
                    "max_candidates": 300, "min_score": 2, "max_iterations": 20,
                    "parallelism": f"slot-sharded x{world}" + (
-                       f", one RCCL all-gather per step of the decodes compacted on the device "
-                       f"({GATHER_PER_SLOT} rows/slot/rank)" if world > 1 else "")},
+                       ", one data-sized RCCL all-gather of the device-compacted decodes per step"
+                       if world > 1 else "")},
         "ldpc_candidates_per_s": cand_per_s,
         "decodes_per_step": decoded,  # successful decodes in one step's batch (every step decodes the same batch)
         "roofline": {"kernel": "k_bp (float64 BP + CRC)", "bound": "fp64-valu",
                      "achieved": ach_tf, "peak": FP64_VECTOR_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": ach_tf / FP64_VECTOR_PEAK_TFLOPS, "traffic": hbm("ft8::k_bp"),
+                     "frac": ach_tf / FP64_VECTOR_PEAK_TFLOPS, "traffic": hbm("ft8::k_bp"), "traffic_source": tsrc,
                      "flops_per_launch": flops, "launch_ms": bp_ms,
-                     "bp_passes_per_launch": cn["passes"] / KT, "candidates_per_launch": cn["candidates"] / KT},
+                     "launch_ms_from": f"wall clock over {R} back-to-back re-launches of the step's k_bp",
+                     "bp_passes_per_launch": cn["passes"] / R, "candidates_per_launch": cn["candidates"] / R},
         "step_hbm": {"what": "BASELINE.md whole-step accounting: slots/s per GPU x B_slot algorithmic bytes "
                              "(the step is FP64-VALU bound in k_bp, so this fraction is low by construction)",
                      "bytes_per_slot": b_slot, "achieved": step_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": step_gbs / HBM_PEAK_GBS},
         "roofline_hbm": {"kernel": "k_stft", "bound": "hbm", "achieved": stft_gbs, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": stft_gbs / HBM_PEAK_GBS, "traffic": hbm("ft8::k_stft"),
+                         "unit": "GB/s", "frac": stft_gbs / HBM_PEAK_GBS,
+                         "traffic": hbm("ft8::k_stft"), "traffic_source": tsrc,
                          "bytes_per_launch": stft_bytes, "launch_ms": stft_ms},
         "stages_ms": stage_ms,
+        "stages_sum_ms": sum(stage_ms.values()),
         "bp_stress": stress,
         "h2d_stream": stream,
         "subtract_redecode": sub,
         "drift_correct": drift,
         "cpu_baseline": cpu,
+        "parity": parity,
+        "reference_measured": REFERENCE_MEASURED,
+        "build_id": _lib.lib().ft8_build_id().decode(),
     }
     if world > 1:
-        totals = gathered[0].cpu().tolist()
-        line["gather"] = {"rows_per_rank": GATHER_PER_SLOT * S,
-                          "bytes_per_rank": GATHER_PER_SLOT * S * 40 + 4 * S + 8,
-                          "decodes_per_rank_last_step": totals,
-                          "truncated": any(t > GATHER_PER_SLOT * S for t in totals)}
+        recs, _, totals = gathered[0]
+        line["gather"] = {"rows_per_rank": int(recs.shape[1]), "bytes_per_rank": int(recs.shape[1]) * 40 + 4 * S + 8,
+                          "decodes_per_rank_last_step": totals.cpu().tolist(), "sized_from_data": True}
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -121,21 +121,51 @@ def lib():
             "ft8_stft_argmax": ([vp, vp, ctypes.c_int, i64, i32, i64, P, vp, vp], ctypes.c_int),
             "ft8_drift_fit": ([vp, i32, vp, i32, i32, i32, DP, vp, vp, vp, i32, vp], ctypes.c_int),
             "ft8_drift_correct": ([vp, vp, ctypes.c_int, i64, i32, i64, DP, vp, vp, vp], ctypes.c_int),
+            "ft8_build_id": ([], ctypes.c_char_p),
+            "ft8_build_flags": ([], ctypes.c_char_p),
+            "ft8_replay_stage": ([vp, i32, i32, vp], ctypes.c_int),
         }
         for name, (args, res) in sig.items():
             fn = getattr(L, name)
             fn.argtypes = args
             fn.restype = res
         _ = dbl
+        built, want = L.ft8_build_id().decode(), source_hash()
+        if want is not None and built != want:
+            raise Ft8Error(
+                f"stale {LIB_PATH}: built from sources {built}, the tree holds {want}; rebuild with "
+                "`python -c 'import __graft_entry__ as g; g.build()'`")
         _lib = L
     return _lib
+
+
+# csrc files hashed into FT8_BUILD_ID, in the Makefile's ID_FILES order
+_ID_FILES = ("capi.hip", "stft.hip", "sync.hip", "bp.hip", "tx.hip", "subtract.hip", "drift.hip",
+             "ft8_internal.h", "ft8_ldpc_tables.h", "tx_device.h", "heap_replay.h", "../../include/ft8hip.h",
+             "Makefile")
+
+
+def source_hash():
+    """SHA-256 prefix of the library's sources as the Makefile computes FT8_BUILD_ID, or None when
+    the sources are not beside the library (an installed copy)."""
+    import hashlib
+    csrc = os.path.join(_HERE, "csrc")
+    paths = [os.path.normpath(os.path.join(csrc, f)) for f in _ID_FILES]
+    if not all(os.path.exists(p) for p in paths):
+        return None
+    h = hashlib.sha256()
+    for p in paths:
+        with open(p, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:32]
 
 
 EXPORTED_SYMBOLS = (
     "ft8_create", "ft8_destroy", "ft8_last_error", "ft8_abi_version", "ft8_limits", "ft8_geometry",
     "ft8_stft", "ft8_sync_select", "ft8_llr", "ft8_normalize", "ft8_bp", "ft8_decode_batch", "ft8_select_warnings",
     "ft8_crc14", "ft8_ldpc_check", "ft8_set_timing", "ft8_get_timing", "ft8_get_counters", "ft8_set_pipeline",
-    "ft8_encode", "ft8_synthesize", "ft8_subtract", "ft8_stft_argmax", "ft8_drift_fit", "ft8_drift_correct")
+    "ft8_encode", "ft8_synthesize", "ft8_subtract", "ft8_stft_argmax", "ft8_drift_fit", "ft8_drift_correct",
+    "ft8_build_id", "ft8_build_flags", "ft8_replay_stage")
 
 
 def limits():
@@ -200,6 +230,12 @@ class Context:
         """ft8_decode_batch chunking over internal streams (n_streams = 0: one chain)."""
         self.check(lib().ft8_set_pipeline(self.handle, int(chunk_slots), int(n_streams), int(bp_waves_per_simd)),
                    "ft8_set_pipeline")
+
+    def replay(self, stage: str, reps: int = 1, stream=None):
+        """ft8_replay_stage: re-launch one kernel of the last ft8_decode_batch `reps` times."""
+        self.check(lib().ft8_replay_stage(self.handle, STAGE_NAMES.index(stage), int(reps),
+                                          stream if stream is not None else stream_handle(self.device)),
+                   "ft8_replay_stage")
 
     def counters(self, reset: bool = False):
         v = (ctypes.c_int64 * 4)()

@@ -187,7 +187,10 @@ class SlotDecoder:
         self.flags = flags
         self.device = _lib.device_index(device)
         self.ctx = _lib.context(self.device)
-        self.cap = int(max_results_per_slot if max_results_per_slot is not None else max(self.max_candidates, 1))
+        # a subtract-and-redecode batch appends up to max_candidates pass-2 records after up to
+        # max_candidates pass-1 records, so its default capacity holds both passes
+        default_cap = max(self.max_candidates, 1) * (2 if flags & _lib.FT8_FLAG_SUBTRACT else 1)
+        self.cap = int(max_results_per_slot if max_results_per_slot is not None else default_cap)
         self._plans = {}
         self._out = None
         self._counts = None
@@ -240,6 +243,12 @@ class SlotDecoder:
         n_slots = len(c)
         recs = out[: n_slots * self.cap * _lib.RESULT_DTYPE.itemsize].cpu().numpy().view(_lib.RESULT_DTYPE)
         recs = recs.reshape(n_slots, self.cap) if n_slots else recs.reshape(0, self.cap)
+        over = np.nonzero(c > self.cap)[0]
+        if over.size:
+            import warnings
+            warnings.warn(f"{over.size} slot(s) decoded more messages than max_results_per_slot={self.cap} "
+                          f"(e.g. slot {int(over[0])}: {int(c[over[0]])}); the records beyond it were dropped",
+                          RuntimeWarning, stacklevel=2)
         return [recs[s, : min(int(c[s]), self.cap)].copy() for s in range(n_slots)]
 
     def decode(self, samples, int16_is_pcm=True):

@@ -10,6 +10,13 @@
 
 #include "ft8_internal.h"
 
+#ifndef FT8_BUILD_ID
+#define FT8_BUILD_ID "unversioned"
+#endif
+#ifndef FT8_BUILD_FLAGS
+#define FT8_BUILD_FLAGS ""
+#endif
+
 using namespace ft8;
 
 namespace {
@@ -69,6 +76,13 @@ struct ft8_ctx {
   std::vector<hipStream_t> streams;
   hipEvent_t fork = nullptr;
   std::vector<hipEvent_t> joins;
+  // the kernels of the last single-chain ft8_decode_batch, for ft8_replay_stage (benchmarking):
+  // valid until the next entry point that may reallocate the context's scratch
+  bool replay_ok = false;
+  StftLaunch last_stft{};
+  SyncLaunch last_sync{};
+  BpLaunch last_bp{};
+  CompactLaunch last_compact{};
 };
 
 namespace {
@@ -352,6 +366,7 @@ int do_stft(ft8_ctx* c, const void* samples, int dtype, int64_t n_samples, int n
   L.window = w->w;
   L.scale = w->scale;
   L.out = d_wf;
+  c->last_stft = L;
   StageTimer tm(c, 0, s);
   hipError_t e = launch_stft(L, s);
   tm.done();
@@ -453,6 +468,7 @@ int sync_select_core(ft8_ctx* c, const void* d_wf, int wf_f64, int n_slots, int 
   L.rowsum = rowsum;
   L.tie = tie;
   L.topk = (p->flags & FT8_FLAG_TOPK) ? 1 : 0;
+  c->last_sync = L;
   StageTimer t1(c, 1, s);
   hipError_t e = launch_score(L, s);
   t1.done();
@@ -560,6 +576,8 @@ int decode_pass(ft8_ctx* c, const void* d_samples, int dtype, int64_t n_samples,
     C.cap = cap;
     C.warn = warn;
     C.tie = tie;
+    c->last_bp = B;
+    c->last_compact = C;
     StageTimer t4(c, 4, cs);
     e = launch_compact(C, cs);
     t4.done();
@@ -569,6 +587,7 @@ int decode_pass(ft8_ctx* c, const void* d_samples, int dtype, int64_t n_samples,
     if ((e = hipEventRecord(c->joins[i], c->streams[i])) != hipSuccess) return hipfail(c, e, "join");
     if ((e = hipStreamWaitEvent(s, c->joins[i], 0)) != hipSuccess) return hipfail(c, e, "join wait");
   }
+  c->replay_ok = n_chunks == 1;
   return FT8_OK;
 }
 
@@ -848,6 +867,7 @@ int ft8_geometry(int32_t fs, int32_t bpt, int32_t sps, int64_t n, int32_t* npers
 
 int ft8_stft(ft8_ctx* c, const void* d_samples, int dtype, int64_t n_samples, int32_t n_slots, int64_t slot_stride,
              const ft8_params* p, void* d_wf, void* stream) {
+  if (c) c->replay_ok = false;
   if (!c || !p || (!d_samples && n_slots > 0) || (!d_wf && n_slots > 0)) return fail(c, FT8_E_ARG, "null argument");
   DeviceGuard dg(c->device);
   return do_stft(c, d_samples, dtype, n_samples, n_slots, slot_stride, p, d_wf, (hipStream_t)stream);
@@ -856,6 +876,7 @@ int ft8_stft(ft8_ctx* c, const void* d_samples, int dtype, int64_t n_samples, in
 int ft8_sync_select(ft8_ctx* c, const void* d_wf, int wf_f64, int32_t n_slots, int32_t T, int32_t F,
                     const ft8_params* p, int32_t* d_cand, double* d_cand_score, int32_t* d_cand_count,
                     void* d_scores, void* stream) {
+  if (c) c->replay_ok = false;
   if (!c || !p || !d_cand_count) return fail(c, FT8_E_ARG, "null argument");
   if (T < 0 || F < 0 || n_slots < 0) return fail(c, FT8_E_ARG, "negative size");
   DeviceGuard dg(c->device);
@@ -865,6 +886,7 @@ int ft8_sync_select(ft8_ctx* c, const void* d_wf, int wf_f64, int32_t n_slots, i
 
 int ft8_llr(ft8_ctx* c, const void* d_wf, int wf_f64, int32_t T, int32_t F, int32_t sps, int32_t bpt,
             const int32_t* d_cand, int32_t n, int normalize, double* d_llr, void* stream) {
+  if (c) c->replay_ok = false;
   if (!c || !d_llr || (!d_cand && n > 0) || sps <= 0 || bpt <= 0) return fail(c, FT8_E_ARG, "bad argument");
   if (n <= 0) return FT8_OK;
   DeviceGuard dg(c->device);
@@ -887,6 +909,7 @@ int ft8_llr(ft8_ctx* c, const void* d_wf, int wf_f64, int32_t T, int32_t F, int3
 }
 
 int ft8_normalize(ft8_ctx* c, const double* d_in, int32_t n, double* d_out, void* stream) {
+  if (c) c->replay_ok = false;
   if (!c || (n > 0 && (!d_in || !d_out))) return fail(c, FT8_E_ARG, "bad argument");
   if (n <= 0) return FT8_OK;
   DeviceGuard dg(c->device);
@@ -904,6 +927,7 @@ int ft8_normalize(ft8_ctx* c, const double* d_in, int32_t n, double* d_out, void
 
 int ft8_bp(ft8_ctx* c, const double* d_llr, int32_t n, int32_t max_iterations, uint8_t* d_plain, ft8_result* d_res,
            void* stream) {
+  if (c) c->replay_ok = false;
   if (!c || (!d_llr && n > 0)) return fail(c, FT8_E_ARG, "bad argument");
   if (n <= 0) return FT8_OK;
   DeviceGuard dg(c->device);
@@ -928,6 +952,7 @@ int ft8_bp(ft8_ctx* c, const double* d_llr, int32_t n, int32_t max_iterations, u
 int ft8_decode_batch(ft8_ctx* c, const void* d_samples, int dtype, int64_t n_samples, int32_t n_slots,
                      int64_t slot_stride, const ft8_params* p, ft8_result* d_out, int32_t* d_counts,
                      int32_t cap, void* stream) {
+  if (c) c->replay_ok = false;
   if (!c || !p || !d_counts || (n_slots > 0 && !d_samples) || n_slots < 0 || cap < 0)
     return fail(c, FT8_E_ARG, "bad argument");
   if (cap > 0 && !d_out) return fail(c, FT8_E_ARG, "null output with positive capacity");
@@ -991,12 +1016,14 @@ int ft8_decode_batch(ft8_ctx* c, const void* d_samples, int dtype, int64_t n_sam
   if ((rc = decode_pass(c, resid, FT8_F32, n_samples, n_slots, n_samples, p, out2, counts2, N, s))) return rc;
   hipError_t e = launch_merge_pass(d_out, d_counts, cap, out1, counts1, N, out2, counts2, N, n_slots, s);
   if (e != hipSuccess) return hipfail(c, e, "merge launch");
+  c->replay_ok = false;
   whole.done();
   return FT8_OK;
 }
 
 int ft8_encode(ft8_ctx* c, const uint8_t* d_msg, int32_t msg_bytes, int32_t n, uint8_t* d_a91, uint8_t* d_codeword,
                uint8_t* d_tones, void* stream) {
+  if (c) c->replay_ok = false;
   if (!c || n < 0 || (n > 0 && !d_msg)) return fail(c, FT8_E_ARG, "bad argument");
   if (msg_bytes != 10 && msg_bytes != 12) return fail(c, FT8_E_ARG, "msg_bytes must be 10 (payload) or 12 (a91)");
   if (n == 0) return FT8_OK;
@@ -1008,6 +1035,7 @@ int ft8_encode(ft8_ctx* c, const uint8_t* d_msg, int32_t msg_bytes, int32_t n, u
 int ft8_synthesize(ft8_ctx* c, const uint8_t* d_tones, const ft8_tx_signal* d_signals, int32_t n_signals,
                    int32_t sample_rate, int32_t style, void* d_out, int out_dtype, int64_t n_samples, int32_t n_slots,
                    int64_t slot_stride, void* stream) {
+  if (c) c->replay_ok = false;
   if (!c || n_signals < 0 || n_slots < 0 || n_samples < 0 || sample_rate <= 0) return fail(c, FT8_E_ARG, "bad argument");
   if (style != FT8_TX_PROTOCOL && style != FT8_TX_REFERENCE) return fail(c, FT8_E_ARG, "unknown ft8_tx_style");
   if (out_dtype != FT8_F32 && out_dtype != FT8_F64 && out_dtype != FT8_C64 && out_dtype != FT8_C128)
@@ -1040,6 +1068,7 @@ int ft8_synthesize(ft8_ctx* c, const uint8_t* d_tones, const ft8_tx_signal* d_si
 int ft8_subtract(ft8_ctx* c, const void* d_samples, int dtype, float* d_residual, int64_t n_samples, int32_t n_slots,
                  int64_t slot_stride, const ft8_params* p, const ft8_result* d_res, const int32_t* d_counts, int32_t cap,
                  void* stream) {
+  if (c) c->replay_ok = false;
   if (!c || !p || n_slots < 0 || cap < 0 || n_samples < 0) return fail(c, FT8_E_ARG, "bad argument");
   if (n_slots == 0 || n_samples == 0) return FT8_OK;
   if (!d_samples || !d_residual || !d_counts || (cap > 0 && !d_res)) return fail(c, FT8_E_ARG, "null argument");
@@ -1051,6 +1080,7 @@ int ft8_subtract(ft8_ctx* c, const void* d_samples, int dtype, float* d_residual
 
 int ft8_stft_argmax(ft8_ctx* c, const void* d_samples, int dtype, int64_t n_samples, int32_t n_slots,
                     int64_t slot_stride, const ft8_params* p, int32_t* d_idx, void* stream) {
+  if (c) c->replay_ok = false;
   if (!c || !p || (n_slots > 0 && (!d_samples || !d_idx))) return fail(c, FT8_E_ARG, "null argument");
   if (n_slots < 0 || n_samples < 0) return fail(c, FT8_E_ARG, "negative size");
   if (n_slots > 1 && slot_stride < n_samples) return fail(c, FT8_E_ARG, "slot_stride < n_samples");
@@ -1061,6 +1091,7 @@ int ft8_stft_argmax(ft8_ctx* c, const void* d_samples, int dtype, int64_t n_samp
 int ft8_drift_fit(ft8_ctx* c, int32_t stage, const int32_t* d_idx, int32_t n_slots, int32_t T, int32_t F,
                   const ft8_drift_params* p, ft8_drift_result* d_res, double* d_metric, int32_t* d_segments,
                   int32_t max_segments, void* stream) {
+  if (c) c->replay_ok = false;
   if (!c || !p) return fail(c, FT8_E_ARG, "null argument");
   if (stage != 1 && stage != 2) return fail(c, FT8_E_ARG, "stage must be 1 or 2");
   if (n_slots < 0 || T < 0 || max_segments < 0) return fail(c, FT8_E_ARG, "negative size");
@@ -1074,6 +1105,7 @@ int ft8_drift_fit(ft8_ctx* c, int32_t stage, const int32_t* d_idx, int32_t n_slo
 int ft8_drift_correct(ft8_ctx* c, const void* d_samples, int dtype, int64_t n_samples, int32_t n_slots,
                       int64_t slot_stride, const ft8_drift_params* p, void* d_out, ft8_drift_result* d_res,
                       void* stream) {
+  if (c) c->replay_ok = false;
   if (!c || !p) return fail(c, FT8_E_ARG, "null argument");
   if (n_slots < 0 || n_samples < 0) return fail(c, FT8_E_ARG, "negative size");
   if (n_slots == 0) return FT8_OK;
@@ -1130,6 +1162,30 @@ int ft8_drift_correct(ft8_ctx* c, const void* d_samples, int dtype, int64_t n_sa
   return e == hipSuccess ? FT8_OK : hipfail(c, e, "derotate launch");
 }
 
+const char* ft8_build_id(void) { return FT8_BUILD_ID; }
+const char* ft8_build_flags(void) { return FT8_BUILD_FLAGS; }
+
+int ft8_replay_stage(ft8_ctx* c, int32_t stage, int32_t reps, void* stream) {
+  if (!c || reps < 0) return fail(c, FT8_E_ARG, "bad argument");
+  if (!c->replay_ok) return fail(c, FT8_E_ARG, "no single-chain ft8_decode_batch to replay");
+  DeviceGuard dg(c->device);
+  hipStream_t s = (hipStream_t)stream;
+  for (int r = 0; r < reps; ++r) {
+    hipError_t e;
+    switch (stage) {
+      case 0: e = launch_stft(c->last_stft, s); break;
+      case 1: e = launch_score(c->last_sync, s); break;
+      case 2: e = launch_select(c->last_sync, s); break;
+      case 3: e = launch_bp(c->last_bp, s); break;
+      case 4: e = launch_compact(c->last_compact, s); break;
+      case 6: e = launch_llr(c->last_bp, s); break;
+      default: return fail(c, FT8_E_ARG, "stage " + std::to_string(stage) + " cannot be replayed");
+    }
+    if (e != hipSuccess) return hipfail(c, e, "replay launch");
+  }
+  return FT8_OK;
+}
+
 int ft8_set_pipeline(ft8_ctx* c, int32_t chunk_slots, int32_t n_streams, int32_t bp_waves_per_simd) {
   if (!c || chunk_slots < 0 || n_streams < 0 || n_streams > 8 || bp_waves_per_simd < 1 || bp_waves_per_simd > 4)
     return fail(c, FT8_E_ARG, "bad pipeline setting");
@@ -1150,6 +1206,7 @@ int ft8_select_warnings(ft8_ctx* c, int32_t* d_out, int32_t n_slots, void* strea
 }
 
 int ft8_crc14(ft8_ctx* c, const uint8_t* d_msg, const int32_t* d_nbits, int32_t n, uint16_t* d_crc, void* stream) {
+  if (c) c->replay_ok = false;
   if (!c || (n > 0 && (!d_msg || !d_nbits || !d_crc))) return fail(c, FT8_E_ARG, "bad argument");
   DeviceGuard dg(c->device);
   hipError_t e = launch_crc14(d_msg, d_nbits, n, d_crc, (hipStream_t)stream);
@@ -1157,6 +1214,7 @@ int ft8_crc14(ft8_ctx* c, const uint8_t* d_msg, const int32_t* d_nbits, int32_t 
 }
 
 int ft8_ldpc_check(ft8_ctx* c, const uint8_t* d_bits, int32_t n, int32_t* d_errors, void* stream) {
+  if (c) c->replay_ok = false;
   if (!c || (n > 0 && (!d_bits || !d_errors))) return fail(c, FT8_E_ARG, "bad argument");
   DeviceGuard dg(c->device);
   hipError_t e = launch_ldpc_check(d_bits, n, d_errors, (hipStream_t)stream);

@@ -52,27 +52,58 @@ def compact_records(records, counts, cap, capacity):
     return dense[:capacity], c.sum()
 
 
-def gather_decodes(records, counts, cap, capacity, group=None):
-    """One all-gather of every rank's decodes, compacted: each rank packs its records into
-    `capacity` dense rows (compact_records) plus its per-slot counts and total into one byte buffer,
-    so the exchange moves capacity*40 + 4*S + 8 bytes per rank instead of S*cap*40.
+def gather_decodes(records, counts, cap, capacity=None, group=None, slot_offset=0):
+    """One all-gather of every rank's decodes, compacted: each rank packs its records into dense
+    rows (compact_records) plus its per-slot counts and total into one byte buffer, so the exchange
+    moves rows*40 + 4*S + 8 bytes per rank instead of S*cap*40.
 
-    Returns (records uint8 [world, capacity, 40], counts int32 [world, S], totals int64 [world]) on
-    every rank; rank r's first min(totals[r], capacity) rows are its decodes in slot order, and
-    totals[r] > capacity flags a truncated rank (raise `capacity`)."""
+    capacity=None (default) sizes the exchange from the data in two phases: an all-gather of the
+    per-rank totals (8 bytes each; one host sync), then exactly max(totals) rows per rank, so no
+    rank is ever truncated whatever the decodes per slot (top-k / subtract-and-redecode batches
+    decode ~28 per slot).  An int capacity keeps a fixed row count (no extra sync); a rank whose
+    total exceeds it is flagged by totals[r] > capacity.
+
+    Returns (records uint8 [world, rows, 40], counts int32 [world, S], totals int64 [world]) on
+    every rank; rank r's first min(totals[r], rows) rows are its decodes in slot order.
+    slot_offset (this rank's first global slot, e.g. shard_range's lo) is added to every record's
+    `slot` field, so gathered records carry global slot indices."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
     S = counts.numel()
+    dev = records.device
+    if capacity is None:
+        mine = counts.to(torch.int64).clamp(0, cap).sum().reshape(1)
+        tot_all = torch.empty(world, dtype=torch.int64, device=dev)
+        dist.all_gather_into_tensor(tot_all, mine, group=group)
+        capacity = int(tot_all.max().item())
     dense, total = compact_records(records, counts, cap, capacity)
+    if slot_offset:
+        ids = dense.view(torch.int32)[:, 2]  # ft8_result.slot (bytes 8..11), rows < total only
+        ids.add_((torch.arange(capacity, device=dev) < total).to(torch.int32) * int(slot_offset))
     nrec = capacity * REC_BYTES
-    buf = torch.empty(nrec + 4 * S + 8, dtype=torch.uint8, device=records.device)
+    buf = torch.empty(nrec + 4 * S + 8, dtype=torch.uint8, device=dev)
     buf[:nrec] = dense.reshape(-1)
     buf[nrec:nrec + 4 * S] = counts.to(torch.int32).contiguous().view(torch.uint8)
     buf[nrec + 4 * S:] = total.reshape(1).view(torch.uint8)
-    out = torch.empty(world * buf.numel(), dtype=torch.uint8, device=records.device).view(world, -1)
+    out = torch.empty(world * buf.numel(), dtype=torch.uint8, device=dev).view(world, -1)
     dist.all_gather_into_tensor(out.view(-1), buf, group=group)
     recs = out[:, :nrec].reshape(world, capacity, REC_BYTES)
     cnts = out[:, nrec:nrec + 4 * S].contiguous().view(torch.int32)
     totals = out[:, nrec + 4 * S:].contiguous().view(torch.int64).reshape(world)
     return recs, cnts, totals
+
+
+def gathered_records(recs, totals):
+    """(records [world, rows, 40], totals [world]) of gather_decodes -> one structured ft8_result
+    array (host) of every rank's decodes, rank-major (i.e. in global slot order when ranks hold
+    contiguous shards); raises if a rank was truncated."""
+    import numpy as np
+    from ._lib import RESULT_DTYPE
+    rows = recs.shape[1]
+    tot = [int(t) for t in totals.cpu().tolist()]
+    if any(t > rows for t in tot):
+        raise RuntimeError(f"gather_decodes truncated: totals {tot} > {rows} rows per rank")
+    r = recs.cpu().numpy()
+    parts = [r[k, :tot[k]].reshape(-1).view(RESULT_DTYPE) for k in range(len(tot))]
+    return np.concatenate(parts) if parts else np.zeros(0, RESULT_DTYPE)

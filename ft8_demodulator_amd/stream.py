@@ -48,6 +48,7 @@ class StreamDecoder:
         self.hout = [torch.empty(self.max_batch * cap, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
         self.hcnt = [torch.empty(self.max_batch, dtype=torch.int32, pin_memory=True) for _ in range(2)]
         self.ready = [None, None]   # compute-stream event: results copied to hout/hcnt[i]
+        self.caller_upload = None   # copy-stream event of an in-place upload of a caller's pinned tensor
 
     def _stage(self, i: int, batch) -> int:
         """Start the upload of a host batch into device buffer i.  A pinned torch tensor is uploaded
@@ -65,6 +66,7 @@ class StreamDecoder:
                 up = torch.cuda.Event()
                 up.record(self.copy_stream)
             self.compute.wait_event(up)
+            self.caller_upload = up  # the caller's buffer is read until this completes
             return nb
         b = np.asarray(batch)
         if b.ndim == 1:
@@ -114,8 +116,13 @@ class StreamDecoder:
         pending = None
         for k, batch in enumerate(batches):
             i = k % 2
+            self.caller_upload = None
             nb = self._stage(i, batch)
             self._launch(i, nb)
+            if self.caller_upload is not None:
+                # a pinned caller tensor is uploaded in place: wait for that upload (it overlaps the
+                # previous batch's decode) before control returns to the caller, who may refill it
+                self.caller_upload.synchronize()
             if pending is not None:
                 yield self._collect(*pending)
             pending = (i, nb)

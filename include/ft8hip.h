@@ -296,6 +296,22 @@ int ft8_drift_correct(ft8_ctx* ctx, const void* d_samples, int dtype, int64_t n_
                       int64_t slot_stride, const ft8_drift_params* p, void* d_out, ft8_drift_result* d_res,
                       void* stream);
 
+/* ---- build provenance --------------------------------------------------------------------- */
+/* SHA-256 prefix of the sources, headers and Makefile the library was compiled from (the Python
+ * binding recomputes it from the tree and refuses a stale library), and the effective compile
+ * flags of every object.  No reference counterpart. */
+const char* ft8_build_id(void);
+const char* ft8_build_flags(void);
+
+/* ---- benchmarking: re-launch one kernel of the last ft8_decode_batch -------------------------
+ * Re-launches, reps times on `stream`, the kernel of `stage` (0 stft, 1 score, 2 select, 6 llr,
+ * 3 bp, 4 compact) exactly as the last single-chain ft8_decode_batch of this context launched it
+ * (same buffers, same arguments; every stage is idempotent on its inputs), so a kernel's duration
+ * can be measured by wall clock over back-to-back launches, without events between stages.  Valid
+ * while the caller's buffers of that call are alive and until any other entry point of this
+ * context runs (FT8_E_ARG otherwise).  No reference counterpart. */
+int ft8_replay_stage(ft8_ctx* ctx, int32_t stage, int32_t reps, void* stream);
+
 /* ---- per-stage device timing (HIP events on the caller's stream) --------------------------- */
 #define FT8_N_STAGES 11 /* 0 stft, 1 score, 2 select, 3 bp, 4 compact, 5 whole decode_batch, 6 llr,
                          7 subtract, 8 drift STFT-argmax, 9 drift fits, 10 drift de-rotation */

@@ -1,10 +1,24 @@
-"""N>1 path on CPU: world_size 2 over gloo -- slot sharding and the record all-gather."""
+"""N>1 path on CPU: world_size 2 over gloo -- slot sharding and the record all-gathers (fixed
+buffers, fixed-capacity compaction and the data-sized two-phase exchange)."""
 import os
 
+import numpy as np
 import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
+
+
+def _records(lo, hi, cap, counts):
+    """Fake ft8_result rows: byte 0 = global slot, bytes 8..11 (slot field) = local slot, byte 28
+    (payload[0]) = row within the slot."""
+    n = hi - lo
+    rec = torch.zeros(n * cap * 40, dtype=torch.uint8)
+    v = rec.view(n, cap, 40)
+    v[:, :, 0] = torch.arange(lo, hi, dtype=torch.uint8)[:, None]
+    v[:, :, 28] = torch.arange(cap, dtype=torch.uint8)[None, :]
+    v.view(n, cap, 10, 4)[:, :, 2, :] = torch.arange(n, dtype=torch.int32)[:, None].view(torch.uint8)[:, None, :]
+    return rec, counts
 
 
 def _worker(rank, world, port, n_slots, q):
@@ -13,20 +27,25 @@ def _worker(rank, world, port, n_slots, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
       try:
-        from ft8_demodulator_amd.distributed import gather_records, shard_range
+        from ft8_demodulator_amd.distributed import (gather_decodes, gather_records, gathered_records,
+                                                      shard_range)
         lo, hi = shard_range(n_slots, rank, world)
         cap = 3
-        rec = torch.zeros((hi - lo) * cap * 40, dtype=torch.uint8)
-        rec.view(hi - lo, cap, 40)[:, :, 0] = torch.arange(lo, hi, dtype=torch.uint8)[:, None]
-        cnt = torch.arange(lo, hi, dtype=torch.int32) % 4
+        rec, cnt = _records(lo, hi, cap, torch.arange(lo, hi, dtype=torch.int32) % 4)
         r_all, c_all = gather_records(rec, cnt)
-        from ft8_demodulator_amd.distributed import gather_decodes
         d_all, dc_all, tot = gather_decodes(rec, cnt, cap, 4)
         compact = [d_all[r, :min(int(tot[r]), 4), 0].tolist() for r in range(world)]
+        # data-sized exchange with many decodes per slot (rank 1: 10 + 11 + 12 + 12 rows > 8 per slot)
+        cap2 = 12
+        rec2, cnt2 = _records(lo, hi, cap2, torch.arange(lo, hi, dtype=torch.int32) + 6)
+        s_all, sc_all, stot = gather_decodes(rec2, cnt2, cap2, slot_offset=lo)
+        flat = gathered_records(s_all, stot)
+        sized = (list(s_all.shape), stot.tolist(), flat["slot"].tolist(), flat["payload"][:, 0].tolist(),
+                 [int(b) for b in flat.view(np.uint8).reshape(-1, 40)[:, 0]])
         q.put((rank, lo, hi, r_all.view(world, hi - lo, cap, 40)[:, :, 0, 0].tolist(), c_all.tolist(),
-               compact, dc_all.tolist(), tot.tolist()))
+               compact, dc_all.tolist(), tot.tolist(), sized))
       except Exception as e:  # noqa: BLE001
-        q.put((rank, "error", repr(e), None, None, None, None, None))
+        q.put((rank, "error", repr(e), None, None, None, None, None, None))
         raise
     finally:
         dist.destroy_process_group()
@@ -54,7 +73,7 @@ def test_gloo_world2_gather():
     for p in ps:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for rank, lo, hi, recs, cnts, compact, dcnts, tot in out:
+    for rank, lo, hi, recs, cnts, compact, dcnts, tot, sized in out:
         assert recs == [[0, 1, 2, 3], [4, 5, 6, 7]]
         assert cnts == [[0, 1, 2, 3], [0, 1, 2, 3]]
         # compacted: slot s contributes min(count, cap) rows tagged s, in slot order; rank 1 holds
@@ -62,3 +81,10 @@ def test_gloo_world2_gather():
         assert dcnts == cnts
         assert tot == [0 + 1 + 2 + 3, 0 + 1 + 2 + 3]
         assert compact == [[1, 2, 2, 3], [5, 6, 6, 7]]
+        # sized: counts 6..13 clamped to cap 12 -> rank 0 holds 6+7+8+9 = 30 rows, rank 1 10+11+12+12 = 45;
+        # the exchange carries exactly 45 rows per rank, nothing is truncated, slots are global
+        shape, stot, slots, rows, tags = sized
+        assert shape == [2, 45, 40] and stot == [30, 45]
+        want = [(s, j) for s in range(8) for j in range(min(6 + s, 12))]
+        assert list(zip(slots, rows)) == want
+        assert tags == slots  # the global slot written into byte 0 agrees with the offset slot field

@@ -270,3 +270,31 @@ def test_make_slots_gpu_matches_cpu(gpu):
     assert [t.payloads for t in tg] == [t.payloads for t in tc]
     assert float((xg0.cpu() - xc).abs().max()) < 1e-5
     assert xg.shape == xc.shape and xg.dtype == gpu.float32
+
+
+def test_subtract_capacity_holds_both_passes(gpu):
+    """decode_ft8_message(subtract=True) with a small max_candidates on crowded slots: pass 1 can fill
+    all max_candidates rows, so the default capacity (2 x max_candidates) must keep every pass-2
+    record; an explicit smaller capacity warns instead of dropping records silently."""
+    import warnings
+    from ft8_demodulator_amd import SlotDecoder, _lib, decode_ft8_message, synth
+    x, _ = synth.make_slots(6, 50, seed=777, device="cuda")
+    N = 12
+    flags = _lib.FT8_FLAG_TOPK | _lib.FT8_FLAG_SUBTRACT
+    dec = SlotDecoder(12000, 2, 2, N, 2, 30, flags=flags)
+    assert dec.cap == 2 * N
+    out, counts = dec.run(x)
+    c = counts.cpu().numpy()
+    assert c.max() > N // 2 and c.max() <= 2 * N
+    recs = dec.records(x)
+    assert [len(r) for r in recs] == list(c)
+    assert any((r["pass_index"] == 1).any() for r in recs)
+    full = decode_ft8_message(x[int(c.argmax())].cpu().numpy(), 12000, max_candidates=N, min_score=2,
+                              max_iterations=30, selection="topk", subtract=True)
+    assert len(full) == int(c.max())
+    small = SlotDecoder(12000, 2, 2, N, 2, 30, flags=flags, max_results_per_slot=2)
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        r2 = small.records(x)
+    assert any("max_results_per_slot=2" in str(m.message) for m in w)
+    assert all(len(r) <= 2 for r in r2)
