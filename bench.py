@@ -400,26 +400,18 @@ def launch_ranks(args):
     return subprocess.call(cmd, env=env)
 
 
-def replay_ms(ctx, stage, reps, torch):
-    """Wall-clock duration of one launch of `stage` of the last ft8_decode_batch: `reps`
-    back-to-back re-launches (ft8_replay_stage) between two synchronisations, no events."""
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    ctx.replay(stage, reps)
-    torch.cuda.synchronize()
-    return (time.perf_counter() - t0) / reps * 1e3
-
-
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    # warm-up: k_bp settles over ~15 launches (2.35 -> 2.02 ms per 256-slot launch as the clocks
+    # settle under the FP64 load; profiles/r2_v1_steps.json), so the timed steps start after 20
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--slots", type=int, default=256, help="slots per GPU per step")
     ap.add_argument("--signals", type=int, default=50)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-slots", type=int, default=256)
-    ap.add_argument("--replays", type=int, default=10, help="back-to-back launches per stage timing")
+    ap.add_argument("--stage-steps", type=int, default=10, help="steps per single-stage event pass")
     ap.add_argument("--no-bp-stress", action="store_true", help="skip the config-4 BP stress leg")
     ap.add_argument("--no-h2d", action="store_true", help="skip the PCIe-inclusive streaming leg")
     ap.add_argument("--no-subtract", action="store_true", help="skip the config-4 subtract-and-redecode leg")
@@ -478,7 +470,7 @@ def main():
     torch.cuda.synchronize()
     dec = SlotDecoder(12000, 2, 2, device=dev, **kw)
     ctx = dec.ctx
-    ctx.set_timing(True)   # allocates the device BP work counters; no events are recorded below
+    ctx.set_timing(True)   # allocates the device BP work counters; no events in the timed loop
     ctx.set_timing(False)
 
     # N > 1: every step ends with the data-sized all-gather of the decodes (totals, then exactly
@@ -506,16 +498,25 @@ def main():
     elapsed = time.perf_counter() - t0
     decoded = int(counts.sum().item())
 
-    # per-kernel durations: each kernel of the last step re-launched back to back (wall clock, no
-    # events); the BP work counters of those k_bp re-launches give its algorithmic FLOPs
-    R = max(1, args.replays)
+    # per-kernel durations inside the real step sequence: one pass of `stage_steps` steps per stage,
+    # with HIP events bracketing only that stage's kernel (the rest of the step runs undisturbed);
+    # the BP work counters of the k_bp pass give its algorithmic FLOPs per launch
+    R = max(1, args.stage_steps)
     stage_ms = {}
     for st in STAGE_ORDER:
+        ctx.timing(reset=True)
         if st == "bp":
             ctx.counters(reset=True)
-        stage_ms[st] = replay_ms(ctx, st, R, torch)
+        ctx.set_timing(True, stages=[st])
+        for _ in range(R):
+            step()
+        torch.cuda.synchronize()
+        ctx.set_timing(False)
+        tm = ctx.timing(reset=True)[st]
+        stage_ms[st] = tm[0] / max(tm[1], 1)
         if st == "bp":
             cn = ctx.counters(reset=True)
+    ctx.set_timing(False, stages=None)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -607,7 +608,7 @@ def main():
                      "achieved": ach_tf, "peak": FP64_VECTOR_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": ach_tf / FP64_VECTOR_PEAK_TFLOPS, "traffic": hbm("ft8::k_bp"), "traffic_source": tsrc,
                      "flops_per_launch": flops, "launch_ms": bp_ms,
-                     "launch_ms_from": f"wall clock over {R} back-to-back re-launches of the step's k_bp",
+                     "launch_ms_from": f"HIP events around k_bp alone in {R} full steps after the timed loop",
                      "bp_passes_per_launch": cn["passes"] / R, "candidates_per_launch": cn["candidates"] / R},
         "step_hbm": {"what": "BASELINE.md whole-step accounting: slots/s per GPU x B_slot algorithmic bytes "
                              "(the step is FP64-VALU bound in k_bp, so this fraction is low by construction)",

@@ -124,6 +124,7 @@ def lib():
             "ft8_build_id": ([], ctypes.c_char_p),
             "ft8_build_flags": ([], ctypes.c_char_p),
             "ft8_replay_stage": ([vp, i32, i32, vp], ctypes.c_int),
+            "ft8_set_timing_stages": ([vp, ctypes.c_uint32], ctypes.c_int),
         }
         for name, (args, res) in sig.items():
             fn = getattr(L, name)
@@ -165,7 +166,7 @@ EXPORTED_SYMBOLS = (
     "ft8_stft", "ft8_sync_select", "ft8_llr", "ft8_normalize", "ft8_bp", "ft8_decode_batch", "ft8_select_warnings",
     "ft8_crc14", "ft8_ldpc_check", "ft8_set_timing", "ft8_get_timing", "ft8_get_counters", "ft8_set_pipeline",
     "ft8_encode", "ft8_synthesize", "ft8_subtract", "ft8_stft_argmax", "ft8_drift_fit", "ft8_drift_correct",
-    "ft8_build_id", "ft8_build_flags", "ft8_replay_stage")
+    "ft8_build_id", "ft8_build_flags", "ft8_replay_stage", "ft8_set_timing_stages")
 
 
 def limits():
@@ -217,7 +218,10 @@ class Context:
             raise MemoryError(text)
         raise Ft8Error(text)
 
-    def set_timing(self, on: bool):
+    def set_timing(self, on: bool, stages=None):
+        """Per-stage HIP events on/off; `stages` (names) limits which kernels are bracketed."""
+        mask = 0xFFFFFFFF if stages is None else sum(1 << STAGE_NAMES.index(s) for s in stages)
+        self.check(lib().ft8_set_timing_stages(self.handle, mask), "ft8_set_timing_stages")
         lib().ft8_set_timing(self.handle, int(bool(on)))
 
     def timing(self, reset: bool = False):

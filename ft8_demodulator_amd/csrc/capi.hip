@@ -66,6 +66,7 @@ struct ft8_ctx {
   int tmpl_key[3] = {0, 0, 0};
   int tmpl_len = 0;
   bool timing = false;
+  uint32_t stage_mask = 0xFFFFFFFFu;  // stages that record events while timing is on
   std::vector<TimedLaunch> pending;
   std::vector<hipEvent_t> pool;
   double ms[FT8_N_STAGES] = {0};
@@ -143,7 +144,7 @@ struct StageTimer {
   hipStream_t s;
   hipEvent_t a = nullptr;
   StageTimer(ft8_ctx* c_, int st, hipStream_t s_) : c(c_), stage(st), s(s_) {
-    if (c->timing) {
+    if (c->timing && ((c->stage_mask >> st) & 1u)) {
       a = get_event(c);
       (void)hipEventRecord(a, s);
     }
@@ -1231,6 +1232,12 @@ int ft8_set_timing(ft8_ctx* c, int enable) {
     hipError_t e = hipMemset(c->stats.p, 0, 4 * sizeof(unsigned long long));
     if (e != hipSuccess) return hipfail(c, e, "stats reset");
   }
+  return FT8_OK;
+}
+
+int ft8_set_timing_stages(ft8_ctx* c, uint32_t mask) {
+  if (!c) return FT8_E_ARG;
+  c->stage_mask = mask;
   return FT8_OK;
 }
 

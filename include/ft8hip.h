@@ -316,6 +316,9 @@ int ft8_replay_stage(ft8_ctx* ctx, int32_t stage, int32_t reps, void* stream);
 #define FT8_N_STAGES 11 /* 0 stft, 1 score, 2 select, 3 bp, 4 compact, 5 whole decode_batch, 6 llr,
                          7 subtract, 8 drift STFT-argmax, 9 drift fits, 10 drift de-rotation */
 int ft8_set_timing(ft8_ctx* ctx, int enable);
+/* which stages record events while timing is enabled (bit s = stage s; default all): timing one
+ * stage at a time brackets only that kernel, so the rest of the step runs undisturbed */
+int ft8_set_timing_stages(ft8_ctx* ctx, uint32_t mask);
 /* accumulated milliseconds and launch counts per stage since the last reset; synchronises. */
 int ft8_get_timing(ft8_ctx* ctx, double* ms, int64_t* launches, int reset);
 /* BP work counters, accumulated while timing is enabled: out4 = {candidates decoded, BP

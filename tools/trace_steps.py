@@ -18,9 +18,10 @@ STEP = ("k_stft", "k_score", "k_select", "k_llr", "k_bp", "k_compact")
 
 
 def short(name):
-    n = name.split("(")[0]
-    n = n.replace("ft8::(anonymous namespace)::", "")
-    return n.split("<")[0]
+    n = name.replace("ft8::(anonymous namespace)::", "").replace("ft8::", "")
+    if n.startswith("void "):
+        n = n[5:]
+    return n.split("(")[0].split("<")[0]
 
 
 def main():
@@ -74,8 +75,16 @@ def main():
         "k_bp_replay_mean_ms": st.mean(bp_replay) if bp_replay else None,
         "k_bp_timed_mean_ms": st.mean(p["kernels_ms"]["k_bp"] for p in per) if per else None,
     }
-    if out["k_bp_replay_mean_ms"]:
-        out["line_vs_trace_bp_ratio"] = line["roofline"]["launch_ms"] / out["k_bp_replay_mean_ms"]
+    if per:
+        names = {"stft": "k_stft", "score": "k_score", "select": "k_select", "llr": "k_llr", "bp": "k_bp",
+                 "compact": "k_compact"}
+        km = out["timed_kernels_ms_mean"]
+        out["line_stage_vs_trace_timed"] = {
+            st: line["stages_ms"][st] / next(v for k, v in km.items() if k.startswith(pre))
+            for st, pre in names.items() if st in line.get("stages_ms", {})}
+        out["line_bp_vs_trace_timed_bp"] = line["roofline"]["launch_ms"] / out["k_bp_timed_mean_ms"]
+        out["trace_frac"] = (line["roofline"]["flops_per_launch"] / (out["k_bp_timed_mean_ms"] * 1e-3) / 1e12
+                             / line["roofline"]["peak"])
     s = json.dumps(out, indent=1)
     if a.out:
         with open(a.out, "w") as f:
