@@ -132,7 +132,8 @@ def lib():
             fn.restype = res
         _ = dbl
         built, want = L.ft8_build_id().decode(), source_hash()
-        if want is not None and built != want:
+        # FT8HIP_ALLOW_STALE=1: A/B tooling only (tools/ab_variants.py loads older builds on purpose)
+        if want is not None and built != want and os.environ.get("FT8HIP_ALLOW_STALE") != "1":
             raise Ft8Error(
                 f"stale {LIB_PATH}: built from sources {built}, the tree holds {want}; rebuild with "
                 "`python -c 'import __graft_entry__ as g; g.build()'`")

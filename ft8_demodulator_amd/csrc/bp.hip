@@ -38,8 +38,6 @@ constexpr int kChkSlots = (FT8_LDPC_M + kWave - 1) / kWave;   // 2
 // Every lane owns kEdgeSlots edges, kVarSlots bits and kChkSlots checks; the tails are padded with
 // dummy edges/bits/checks that read and write only padding slots of the LDS arrays, so the three
 // phases are branch-free and the per-lane chains (18 IEEE divisions per sweep) interleave.
-constexpr int kEdgePad = kEdgeSlots * kWave;   // 576: tov/toc slots 522.. are padding
-constexpr int kVarPad = kVarSlots * kWave;     // 192: c/bits slots 174.. are padding
 
 #ifndef BP_DIV_GROUP
 #define BP_DIV_GROUP 3
@@ -102,11 +100,14 @@ __device__ __forceinline__ double pymax4(double a, double b, double c, double d)
 // b = -2 y (exact) and scales the quotient.
 template <int N, bool NEG2 = false>
 __device__ __forceinline__ void div_rn(double* q, const double* x, const double* y_in) {
-  bool safe = true;  // |x| < 2^900 always holds here (clamped / bounded inputs); NaN fails the test
+  // |x| < 2^900 always holds here (clamped / bounded inputs).  A NaN numerator yields NaN on either
+  // path (only its payload could differ, which no later comparison or clip can observe), so the
+  // test is on the smallest |x| alone: two v_min + one compare per group, and one ballot
+  double mn = __builtin_fabs(x[0]);
 #pragma unroll
-  for (int i = 0; i < N; ++i) safe = safe && (__builtin_fabs(x[i]) >= 0x1p-960);
+  for (int i = 1; i < N; ++i) mn = __builtin_fmin(mn, __builtin_fabs(x[i]));
   double r[N], e[N], m[N];
-  if (__all(safe)) {
+  if (__ballot(mn >= 0x1p-960) == __builtin_amdgcn_read_exec()) {
 #pragma unroll
     for (int i = 0; i < N; ++i) r[i] = __builtin_amdgcn_rcp(y_in[i]);
 #pragma unroll
@@ -158,148 +159,125 @@ __device__ __forceinline__ void div_rn(double* q, const double* x, const double*
   (void)f0;
 }
 
+// ---- k_bp message layout ---------------------------------------------------------------------
 // One LDS array holds both message sets: a sweep phase loads everything it needs before it stores
-// (the workgroup is one lockstep wave), so toc can overwrite tov in place and vice versa.
+// (the workgroup is one lockstep wave), so toc overwrites tov in place and vice versa.
 //
-// Dense blocked layout (576 float64 = 9 slots of 64 lanes): the 83 check rows are packed first-fit
-// in check order into 18 blocks of 32 positions, rows never straddling a block; position 31 of
-// every block (lanes 31 and 63 of every slot) holds a constant 1.0, the missing sixth product
-// factor of the degree-6 rows of that block; the 36 unused positions are padding.  Messages are 8
-// bytes apart, so the edge-major loads and stores use all 64 LDS banks (the former interleaved
-// layout, edge e at msg[2e] beside a 1.0, used half of them).  The constant lanes never store; the
-// padding positions' cv entries point at a constant row (product 1.0), so every value a division
-// sees stays finite and non-zero.
-constexpr int kZeroBit = 255;  // bits[255] is never written: the padding checks' variable
-constexpr int kBlocks = kEdgePad / 32;   // 18
-constexpr int kPoffD7 = 0;               // poff[q]: degree-7 row, edge at row position q
-constexpr int kPoffD6 = 7;               // poff[7 + 31 q + rb]: degree-6 row starting rb into its block
-constexpr int kPoffOne = 7 + 31 * 6;     // all-zero offsets: six reads of the same 1.0
-constexpr int kPoffN = kPoffOne + 1;
-struct WaveLds {
-  double msg[kEdgePad];            // tov between sweeps; V->C arguments, then toc, within a sweep
-  uint64_t poff[kPoffN];           // byte offsets of the 6 product factors from the row base
-  uint8_t bits[256];               // hard decision of every variable (last evaluated sweep)
-  uint8_t a91[16];
-};
-static_assert(kEdgePad == 576 && kBlocks == 18, "blocked message layout assumes 9 edge slots");
+// Row-position-major layout.  Checks are renumbered degree-7 first (m' = 0..23 the degree-7 rows,
+// 24..82 the degree-6 rows, each group in check order).  The message of edge (m', q), q being the
+// edge's position in its check's row (the reference's n_idx, ldpc_decoder.py:85-87, 103-105), lives
+// at index q * 83 + m' (q < 6) or 498 + m' (q = 6, m' < 24); indices 522..583 hold the constant
+// 1.0 that stands in for a degree-6 row's missing seventh factor (1.0 * t == t exactly).  Hence:
+//   * factor f of row m' sits at byte 8 m' + 664 f from the array: a row base plus a compile-time
+//     immediate, so the check products need no per-factor address arithmetic;
+//   * edge-major phases (fast_tanh, products, fast_atanh) own index lane + 64 i: the lane address
+//     plus an immediate;
+//   * edge slot i (indices 64 i .. 64 i + 63) holds one row position q, or two adjacent ones qa and
+//     qa + 1 (83 > 64).  The product of "every factor but q" in row order then has, at chain
+//     position qa, t[qa + 1] for the q = qa lanes and t[qa] for the q = qa + 1 lanes -- one
+//     per-lane address; every other factor is common to both groups.
+// The per-variable (174 x 3 edge) addresses of the variable-major phase are per-lane tables.
+constexpr int kM7 = 24;                              // degree-7 checks (FT8 LDPC(174,91))
+constexpr int kQS = FT8_LDPC_M;                      // index stride of one row position (83)
+constexpr int kQ6 = 6 * kQS;                         // first index of row position 6 (498)
+constexpr int kMsgN = 584;                           // 498 + 83 = 581 used, rounded to 8
+constexpr int kOne = kMsgN - 1;                      // a constant 1.0 (padding variables read it)
+constexpr int kHdr = 1024;                           // LDS bytes before msg (lane addr - 664 > 0)
+static_assert(kEdgeSlots * kWave <= kMsgN && kQ6 + kM7 == FT8_LDPC_E, "row-major message layout");
 
-// Per-lane tables (registers, loaded once per wave).  A sweep runs in two layouts:
-//   variable-major (3 slots, variable n = lane + 64 j): hard decision and variable->check sums
-//     va: LDS byte address of the variable's 1st edge message | 2nd edge << 16 (check order)
-//     vb: LDS byte address of its 3rd edge message
-//   edge-major (9 slots, position p = lane + 64 i): fast_tanh, check products, fast_atanh
-//     cv: LDS byte address of the row base | LDS address of its poff entry << 16
-//   check-major (2 slots, check m = lane + 64 k): parity
-//     pk: the check's variables, one byte each (7; a degree-6 check's 7th is kZeroBit)
+__host__ __device__ constexpr int q_of(int idx) { return idx < kQ6 ? idx / kQS : 6; }
+__host__ __device__ constexpr int qa_of(int i) { return q_of(kWave * i); }
+__host__ __device__ constexpr bool mixed_slot(int i) { return q_of(kWave * i + kWave - 1) != q_of(kWave * i); }
+// first lane of slot i whose row position is qa + 1 (mixed slots)
+__host__ __device__ constexpr int hi_lane(int i) { return kQS * (qa_of(i) + 1) - kWave * i; }
+// byte offset, from a lane's row base register, of the row base itself for slot i's lanes
+// (index of factor 0 of the lane's row = lane + 64 i - 83 q)
+__host__ __device__ constexpr int row_off(int i) { return 8 * (kWave * i - kQS * qa_of(i)); }
+
+struct WaveLds {
+  uint8_t bits[256];               // hard decision of every variable (written once per candidate)
+  uint8_t a91[16];
+  uint8_t rank[FT8_LDPC_M];        // prologue scratch: check m -> m'
+  uint8_t chk_of[FT8_LDPC_M];      // prologue scratch: m' -> m
+  uint8_t pad_[kHdr - 256 - 16 - 2 * FT8_LDPC_M];
+  double msg[kMsgN];               // tov between sweeps; V->C arguments, then toc, within a sweep
+};
+static_assert(offsetof(WaveLds, msg) == kHdr, "msg follows the header");
+
+// Per-lane tables (registers, built once per wave).
+//   va[j], vb[j]: variable n = lane + 64 j (variable-major phase): LDS byte addresses of its three
+//                 edge messages in the reference's kFTX_LDPC_Mn order (va: 1st | 2nd << 16, vb: 3rd)
+//   h[k][j]:      check m' = lane + 64 k (parity): its variables as a 174-bit mask, 64-bit word j
+//                 (lo, hi) -- the parity is popcount(h & hard decisions) from wave ballots
 struct WaveTables {
   uint32_t va[kVarSlots];
   uint32_t vb[kVarSlots];
-  uint32_t cv[kEdgeSlots];
-  uint32_t pk[kChkSlots][2];
+  uint32_t h[kChkSlots][kVarSlots][2];
 };
+
+// one ds_read_b64 with the offset as its immediate (volatile: the compiler would otherwise pair
+// factors into ds_read2_b64, whose 8-bit offsets cannot span a row and cost a VALU add per pair)
+__device__ __forceinline__ double ldv(uint32_t addr) {
+  return *(const volatile __attribute__((address_space(3))) double*)(uintptr_t)addr;
+}
 
 __device__ __forceinline__ uint32_t lds_addr(const void* p) {
   return (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const void*)p;
 }
 
-__device__ __forceinline__ bool const_pos(int p) { return (p & 31) == 31; }
-
-// Builds the per-lane tables, the poff entries and the mask of this lane's padding positions
-// (bit i: position lane + 64 i).  The msg array serves as scratch for the row layout first.
-__device__ uint32_t load_tables(WaveTables& t, WaveLds& L, int lane) {
-  int16_t* rowpos = reinterpret_cast<int16_t*>(&L.msg[0]);            // [83] row start position
-  int16_t* pos2edge = reinterpret_cast<int16_t*>(&L.msg[0]) + 128;    // [576] edge at position, -1
-  if (lane == 0) {  // first fit in check order: 18 blocks of 31 usable positions
-    int fill[kBlocks];
-    for (int b = 0; b < kBlocks; ++b) fill[b] = 0;
+__device__ void load_tables(WaveTables& t, WaveLds& L, int lane) {
+  if (lane == 0) {  // degree-7 rows first, each group in check order
+    int c7 = 0, c6 = kM7;
     for (int m = 0; m < FT8_LDPC_M; ++m) {
-      const int d = kChkStartD[m + 1] - kChkStartD[m];
-      int b = 0;
-      while (fill[b] + d > 31) ++b;  // always found: the packing of the FT8 code fits 18 blocks
-      rowpos[m] = (int16_t)(32 * b + fill[b]);
-      fill[b] += d;
+      const int r = (kChkStartD[m + 1] - kChkStartD[m]) == 7 ? c7++ : c6++;
+      L.rank[m] = (uint8_t)r;
+      L.chk_of[r] = (uint8_t)m;
     }
   }
-  for (int p = lane; p < kEdgePad; p += kWave) pos2edge[p] = -1;
   __syncthreads();
-  for (int e = lane; e < FT8_LDPC_E; e += kWave) {
-    const int m = kEdgeChkD[e];
-    pos2edge[rowpos[m] + (e - kChkStartD[m])] = (int16_t)e;
-  }
-  __syncthreads();
-  const uint32_t msg0 = lds_addr(&L.msg[0]), poff0 = lds_addr(&L.poff[0]);
-  const uint32_t one = msg0 + 8u * 31u;  // a constant 1.0
-  auto pos_of = [&](int e) -> uint32_t {
-    const int m = kEdgeChkD[e];
-    return (uint32_t)(rowpos[m] + (e - kChkStartD[m]));
+  const uint32_t msg0 = lds_addr(&L.msg[0]);
+  auto addr_of = [&](int e) -> uint32_t {  // edge (CSR index) -> LDS byte address of its message
+    const int m = kEdgeChkD[e], q = e - kChkStartD[m], r = L.rank[m];
+    return msg0 + 8u * (uint32_t)(q < 6 ? q * kQS + r : kQ6 + r);
   };
 #pragma unroll
   for (int j = 0; j < kVarSlots; ++j) {
     const int n = lane + kWave * j;
     if (n < FT8_LDPC_N) {
-      t.va[j] = (msg0 + 8u * pos_of(kVarEdgeD[3 * n])) | ((msg0 + 8u * pos_of(kVarEdgeD[3 * n + 1])) << 16);
-      t.vb[j] = msg0 + 8u * pos_of(kVarEdgeD[3 * n + 2]);
+      t.va[j] = addr_of(kVarEdgeD[3 * n]) | (addr_of(kVarEdgeD[3 * n + 1]) << 16);
+      t.vb[j] = addr_of(kVarEdgeD[3 * n + 2]);
     } else {  // padding variable: reads the constant, never stores (see the sweep)
+      const uint32_t one = msg0 + 8u * kOne;
       t.va[j] = one | (one << 16);
       t.vb[j] = one;
     }
   }
-  uint32_t padmask = 0;
-#pragma unroll
-  for (int i = 0; i < kEdgeSlots; ++i) {
-    const int p = lane + kWave * i;
-    const int e = pos2edge[p];
-    if (e >= 0) {
-      const int m = kEdgeChkD[e];
-      const int s = kChkStartD[m], d = kChkStartD[m + 1] - s;
-      const int r = rowpos[m], q = e - s;
-      const uint32_t entry = d == 7 ? (uint32_t)(kPoffD7 + q) : (uint32_t)(kPoffD6 + 31 * q + (r & 31));
-      t.cv[i] = (msg0 + 8u * (uint32_t)r) | ((poff0 + 8u * entry) << 16);
-    } else {
-      t.cv[i] = one | ((poff0 + 8u * kPoffOne) << 16);
-      if (!const_pos(p)) padmask |= 1u << i;
-    }
-  }
 #pragma unroll
   for (int k = 0; k < kChkSlots; ++k) {
-    const int m = lane + kWave * k;
-    uint32_t w[2] = {0, 0};
-    for (int q = 0; q < 7; ++q) {
-      uint32_t v = kZeroBit;
-      if (m < FT8_LDPC_M) {
-        const int s = kChkStartD[m], d = kChkStartD[m + 1] - s;
-        if (q < d) v = kEdgeVarD[s + q];
-      }
-      w[q >> 2] |= v << (8 * (q & 3));
-    }
-    t.pk[k][0] = w[0];
-    t.pk[k][1] = w[1];
-  }
-  // poff entries: byte f = 8 * (row position of product factor f): positions f + (f >= q) in row
-  // order; a degree-6 row's sixth factor is its block's constant at 31 - rb positions from the base
-  for (int x = lane; x < kPoffN; x += kWave) {
-    uint64_t w = 0;
-    if (x < kPoffD6) {
-      const int q = x;
-      for (int f = 0; f < 6; ++f) w |= (uint64_t)(8 * (f + (f >= q))) << (8 * f);
-    } else if (x < kPoffOne) {
-      const int q = (x - kPoffD6) / 31, rb = (x - kPoffD6) % 31;
-      for (int f = 0; f < 6; ++f) {
-        const int off = f == 5 ? 8 * (31 - rb) : 8 * (f + (f >= q));
-        w |= (uint64_t)off << (8 * f);
+    const int mp = lane + kWave * k;
+#pragma unroll
+    for (int j = 0; j < kVarSlots; ++j) t.h[k][j][0] = t.h[k][j][1] = 0;
+    if (mp < FT8_LDPC_M) {
+      const int m = L.chk_of[mp];
+      for (int e = kChkStartD[m]; e < kChkStartD[m + 1]; ++e) {
+        const int v = kEdgeVarD[e];
+#pragma unroll
+        for (int j = 0; j < kVarSlots; ++j)
+#pragma unroll
+          for (int w = 0; w < 2; ++w)
+            if (v >> 5 == 2 * j + w) t.h[k][j][w] |= 1u << (v & 31);
       }
     }
-    L.poff[x] = w;
   }
-  __syncthreads();  // scratch reads done before the caller initialises msg
+  for (int x = FT8_LDPC_E + lane; x < kMsgN; x += kWave) L.msg[x] = 1.0;  // the constants, once
+  __syncthreads();
   // keep the tables in registers: opaque values cannot be rematerialised from memory in the loop
 #pragma unroll
   for (int j = 0; j < kVarSlots; ++j) asm volatile("" : "+v"(t.va[j]), "+v"(t.vb[j]));
 #pragma unroll
-  for (int i = 0; i < kEdgeSlots; ++i) asm volatile("" : "+v"(t.cv[i]));
+  for (int k = 0; k < kChkSlots; ++k)
 #pragma unroll
-  for (int k = 0; k < kChkSlots; ++k) asm volatile("" : "+v"(t.pk[k][0]), "+v"(t.pk[k][1]));
-  return padmask;
+    for (int j = 0; j < kVarSlots; ++j) asm volatile("" : "+v"(t.h[k][j][0]), "+v"(t.h[k][j][1]));
 }
 
 struct BpArgs {
@@ -544,12 +522,14 @@ __global__ __launch_bounds__(kWave, BP_WAVES_PER_EU) void k_bp(BpArgs a) {
   __shared__ WaveLds L;
   const int lane = threadIdx.x;
   WaveTables tb;
-  const uint32_t padmask = load_tables(tb, L, lane);
-  for (int n = lane; n < 256; n += kWave) L.bits[n] = 0;
-  // constant lanes (position 31 of a block) never store a message; padding variables (variable
-  // slot 2, lanes >= 46) never store their V->C arguments
-  const bool st_lane = !const_pos(lane);
+  load_tables(tb, L, lane);
+  // padding variables (variable slot 2, lanes >= 46) never store their V->C arguments
   const bool var2 = lane + kWave * (kVarSlots - 1) < FT8_LDPC_N;
+  const uint64_t var2_mask = (1ull << (FT8_LDPC_N - kWave * (kVarSlots - 1))) - 1ull;
+  // the lane's message address in the edge-major phases (slot i: + 512 i) and the row-base
+  // registers of the two lane groups of a mixed slot (q = qa: la, q = qa + 1: la - 664)
+  uint32_t la = lds_addr(&L.msg[0]) + 8u * (uint32_t)lane;
+  asm volatile("" : "+v"(la));  // one register (the generic->LDS cast carries a null test)
 
   // work counters, per wave; flushed once when the wave retires (same-address atomics per
   // candidate would serialise in L2)
@@ -580,31 +560,26 @@ __global__ __launch_bounds__(kWave, BP_WAVES_PER_EU) void k_bp(BpArgs a) {
 
     // ---- belief propagation (ldpc_decoder.py:54-113) ----------------------------------------
     // One sweep = the reference iteration.  (A) variable-major: each lane reads its variables'
-    // three tov, forms the hard decision c + ((t0 + t1) + t2) and the three variable->check sums
-    // (c + t_a) + t_b, and writes the clipped -T/2 into each edge's slot; (B) parity per check from
-    // the decision bytes; (C) edge-major: fast_tanh -> toc; (D) check products -> fast_atanh -> tov.
-    // tov = 0 on every edge; the constants and the padding positions hold 1.0 (the opaque mask
-    // keeps the nine initial values from being hoisted out of the candidate loop and spilled)
-    uint32_t pm = padmask | (const_pos(lane) ? 0x1FFu : 0u);
-    asm volatile("" : "+v"(pm));
+    // three tov, forms the hard decision c + ((t0 + t1) + t2) (a wave ballot per variable slot)
+    // and the three variable->check sums (c + t_a) + t_b, and writes the clipped -T/2 into each
+    // edge's slot; (B) parity of every check from the ballots; (C) edge-major: fast_tanh -> toc;
+    // (D) check products -> fast_atanh -> tov.
+    // tov = 0 on every real edge (indices 0..521; the constants above never change)
 #pragma unroll
-    for (int i = 0; i < kEdgeSlots; ++i) L.msg[lane + kWave * i] = ((pm >> i) & 1u) ? 1.0 : 0.0;
-    for (int n = lane; n < kVarPad; n += kWave) L.bits[n] = 0;  // the hard decision if no sweep runs
+    for (int i = 0; i < kEdgeSlots; ++i)
+      if (i < kEdgeSlots - 1 || lane + kWave * i < FT8_LDPC_E)
+        *(__attribute__((address_space(3))) double*)(uintptr_t)(la + 512u * i) = 0.0;
     __syncthreads();
+    uint64_t hd[kVarSlots] = {0, 0, 0};  // hard decisions of the last evaluated sweep (ballots)
     int min_errors = FT8_LDPC_M;
     int entered = 0, passes = 0;
     for (int iter = 0; iter < a.max_iterations; ++iter) {
       entered++;
-      // re-opaque the tables every sweep: otherwise the compiler hoists the derived LDS addresses
-      // out of the loop (spilling); recomputing them is one integer op each
+      // re-opaque the tables every sweep: otherwise the compiler hoists derived addresses out of
+      // the loop (spilling); recomputing them is one integer op each
 #pragma unroll
       for (int j = 0; j < kVarSlots; ++j) asm volatile("" : "+v"(tb.va[j]), "+v"(tb.vb[j]));
-#pragma unroll
-      for (int i = 0; i < kEdgeSlots; ++i) asm volatile("" : "+v"(tb.cv[i]));
-#pragma unroll
-      for (int k = 0; k < kChkSlots; ++k) asm volatile("" : "+v"(tb.pk[k][0]), "+v"(tb.pk[k][1]));
       // (A) hard decision + variable -> check arguments
-      uint64_t any = 0;
 #pragma unroll
       for (int j = 0; j < kVarSlots; ++j) {
         const uint32_t a0 = tb.va[j] & 0xFFFFu, a1 = tb.va[j] >> 16, a2 = tb.vb[j];
@@ -613,10 +588,7 @@ __global__ __launch_bounds__(kWave, BP_WAVES_PER_EU) void k_bp(BpArgs a) {
         const double t2 = *(lds_f64*)(uintptr_t)a2;
         const double c = cv_[j];
         // messages = codeword + sum(tov, axis=1) (ldpc_decoder.py:72-73)
-        const bool bit = (c + ((t0 + t1) + t2)) > 0.0;
-        const uint64_t bal = __ballot(bit);
-        any |= j == kVarSlots - 1 ? bal & ((1ull << (FT8_LDPC_N - kWave * (kVarSlots - 1))) - 1ull) : bal;
-        L.bits[lane + kWave * j] = (uint8_t)bit;
+        hd[j] = __ballot((c + ((t0 + t1) + t2)) > 0.0);
         // Tnm = codeword[n] + the other two tov in check order (ldpc_decoder.py:90-96)
         const double c0 = c + t0;
         const double T0 = (c + t1) + t2, T1 = c0 + t2, T2 = c0 + t1;
@@ -627,17 +599,21 @@ __global__ __launch_bounds__(kWave, BP_WAVES_PER_EU) void k_bp(BpArgs a) {
           *(__attribute__((address_space(3))) double*)(uintptr_t)a2 = __builtin_fmin(__builtin_fmax(-T2 / 2, -4.97), 4.97);
         }
       }
+      hd[kVarSlots - 1] &= var2_mask;
       sweep_sync();
       // all-zero hard decision -> stop (ldpc_decoder.py:76-78)
-      if (any == 0) break;
-      // (B) parity check (ldpc_check, ldpc_decoder.py:33-52)
+      if ((hd[0] | hd[1] | hd[2]) == 0) break;
+      // (B) parity check (ldpc_check, ldpc_decoder.py:33-52): popcount of (row mask & decisions)
       int errs = 0;
 #pragma unroll
       for (int k = 0; k < kChkSlots; ++k) {
-        unsigned par = 0;
+        uint32_t x = 0;
 #pragma unroll
-        for (int q = 0; q < 7; ++q) par ^= L.bits[(tb.pk[k][q >> 2] >> (8 * (q & 3))) & 0xFFu];
-        errs += __popcll(__ballot(par & 1u));
+        for (int j = 0; j < kVarSlots; ++j) {
+          x = __builtin_amdgcn_bitop3_b32(tb.h[k][j][0], (uint32_t)hd[j], x, 0x6a);          // (h & d) ^ x
+          x = __builtin_amdgcn_bitop3_b32(tb.h[k][j][1], (uint32_t)(hd[j] >> 32), x, 0x6a);
+        }
+        errs += __popcll(__ballot(__builtin_popcount(x) & 1));
       }
       if (errs < min_errors) {
         min_errors = errs;
@@ -645,7 +621,7 @@ __global__ __launch_bounds__(kWave, BP_WAVES_PER_EU) void k_bp(BpArgs a) {
       }
       double x[kEdgeSlots];
 #pragma unroll
-      for (int i = 0; i < kEdgeSlots; ++i) x[i] = L.msg[lane + kWave * i];
+      for (int i = 0; i < kEdgeSlots; ++i) x[i] = *(lds_f64*)(uintptr_t)(la + 512u * i);
       // variable -> check messages: toc = fast_tanh(-Tnm / 2), three interleaved divisions at a time
 #pragma unroll
       for (int g = 0; g < kEdgeSlots; g += kDivGroup) {
@@ -658,25 +634,37 @@ __global__ __launch_bounds__(kWave, BP_WAVES_PER_EU) void k_bp(BpArgs a) {
         }
         div_rn<kDivGroup>(&x[g], na, nb);
       }
-      if (st_lane) {
 #pragma unroll
-        for (int i = 0; i < kEdgeSlots; ++i) L.msg[lane + kWave * i] = x[i];
-      }
+      for (int i = 0; i < kEdgeSlots; ++i)
+        if (i < kEdgeSlots - 1 || lane + kWave * i < FT8_LDPC_E)
+          *(__attribute__((address_space(3))) double*)(uintptr_t)(la + 512u * i) = x[i];
       sweep_sync();
       // check -> variable messages: tov = -2 fast_atanh(prod of the other toc of the check, in row
-      // order, from 1.0).  The six factor addresses are the row address plus the bytes of the
-      // edge's poff word (one SDWA add each); 1.0 * t0 == t0, so the product starts at factor 0.
+      // order, from 1.0; 1.0 * t0 == t0, so the product starts at the first factor)
 #pragma unroll
       for (int i = 0; i < kEdgeSlots; ++i) {
-        const uint32_t v = tb.cv[i];
-        const uint64_t pk = *(lds_u64*)(uintptr_t)(v >> 16);
-        const uint32_t row = v & 0xFFFFu;
+        const int qa = qa_of(i);
+        const bool mx = mixed_slot(i);
+        const bool hi = mx && lane >= hi_lane(i);
+        // row base of the lane (factor 0 of its row): la + row_off(i) for q = qa, 664 less for qa + 1
+        const uint32_t rb = hi ? la - 664u : la;
         double p = 0.0;
+        bool first = true;
 #pragma unroll
-        for (int f = 0; f < 6; ++f) {
-          const uint32_t off = (uint32_t)(pk >> (8 * f)) & 0xFFu;
-          const double t = *(lds_f64*)(uintptr_t)(row + off);
-          p = f == 0 ? t : p * t;
+        for (int f = 0; f < 7; ++f) {
+          double t;
+          if (mx && f == qa) {        // t[qa + 1] (q = qa lanes) or t[qa] (q = qa + 1 lanes)
+            const uint32_t pa = hi ? rb : rb + 664u;
+            t = ldv(pa + (uint32_t)(row_off(i) + 664 * qa));
+          } else if (mx && f == qa + 1) {
+            continue;
+          } else if (!mx && f == qa) {
+            continue;
+          } else {
+            t = ldv(rb + (uint32_t)(row_off(i) + 664 * f));
+          }
+          p = first ? t : p * t;
+          first = false;
         }
         x[i] = p;
         // bound how far the scheduler hoists these loads (register pressure)
@@ -695,19 +683,22 @@ __global__ __launch_bounds__(kWave, BP_WAVES_PER_EU) void k_bp(BpArgs a) {
         }
         div_rn<kDivGroup, true>(&x[g], na, nb);  // tov = -2 fast_atanh(Tmn)
       }
-      if (st_lane) {
 #pragma unroll
-        for (int i = 0; i < kEdgeSlots; ++i) L.msg[lane + kWave * i] = x[i];
-      }
+      for (int i = 0; i < kEdgeSlots; ++i)
+        if (i < kEdgeSlots - 1 || lane + kWave * i < FT8_LDPC_E)
+          *(__attribute__((address_space(3))) double*)(uintptr_t)(la + 512u * i) = x[i];
       passes++;
       sweep_sync();
     }
-    // bits[] holds the hard decision of the last evaluated sweep
+    // the hard decision of the last evaluated sweep (all zero if no sweep ran)
+#pragma unroll
+    for (int j = 0; j < kVarSlots; ++j) L.bits[lane + kWave * j] = (uint8_t)((hd[j] >> lane) & 1u);
     __syncthreads();
     st_cand++;
     st_iter += entered;
     st_pass += passes;
     st_conv += min_errors == 0;
+
 
     // ---- outputs ------------------------------------------------------------------------------
     if (a.plain_out)

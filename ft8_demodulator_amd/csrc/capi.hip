@@ -554,7 +554,7 @@ int decode_pass(ft8_ctx* c, const void* d_samples, int dtype, int64_t n_samples,
     B.res = (ft8_result*)c->res_all.p + (size_t)c0 * N;
     B.work = (unsigned*)c->work.p + k;
     B.stats = (unsigned long long*)c->stats.p;
-    B.grid_waves = n_str > 0 ? c->bp_waves : 4;
+    B.grid_waves = n_str > 0 ? c->bp_waves : 8;  // clamped to the kernel's BP_WAVES_PER_EU
     B.tie = tie;
     B.warn = warn;
     B.tie_scores = (const float*)((char*)c->scores.p + esz * (size_t)c0 * gr.NT * gr.NF);
