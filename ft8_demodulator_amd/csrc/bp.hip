@@ -209,8 +209,15 @@ static_assert(offsetof(WaveLds, msg) == kHdr, "msg follows the header");
 //                 edge messages in the reference's kFTX_LDPC_Mn order (va: 1st | 2nd << 16, vb: 3rd)
 //   h[k][j]:      check m' = lane + 64 k (parity): its variables as a 174-bit mask, 64-bit word j
 //                 (lo, hi) -- the parity is popcount(h & hard decisions) from wave ballots
+#ifndef BP_VA_FULL
+#define BP_VA_FULL 1  // full addresses: no extraction ops in phase A (110 VGPRs; 0 = packed 16-bit pairs)
+#endif
 struct WaveTables {
+#if BP_VA_FULL
+  uint32_t va[kVarSlots], va1[kVarSlots];
+#else
   uint32_t va[kVarSlots];
+#endif
   uint32_t vb[kVarSlots];
   uint32_t h[kChkSlots][kVarSlots][2];
 };
@@ -244,11 +251,20 @@ __device__ void load_tables(WaveTables& t, WaveLds& L, int lane) {
   for (int j = 0; j < kVarSlots; ++j) {
     const int n = lane + kWave * j;
     if (n < FT8_LDPC_N) {
+#if BP_VA_FULL
+      t.va[j] = addr_of(kVarEdgeD[3 * n]);
+      t.va1[j] = addr_of(kVarEdgeD[3 * n + 1]);
+#else
       t.va[j] = addr_of(kVarEdgeD[3 * n]) | (addr_of(kVarEdgeD[3 * n + 1]) << 16);
+#endif
       t.vb[j] = addr_of(kVarEdgeD[3 * n + 2]);
     } else {  // padding variable: reads the constant, never stores (see the sweep)
       const uint32_t one = msg0 + 8u * kOne;
+#if BP_VA_FULL
+      t.va[j] = t.va1[j] = one;
+#else
       t.va[j] = one | (one << 16);
+#endif
       t.vb[j] = one;
     }
   }
@@ -274,6 +290,10 @@ __device__ void load_tables(WaveTables& t, WaveLds& L, int lane) {
   // keep the tables in registers: opaque values cannot be rematerialised from memory in the loop
 #pragma unroll
   for (int j = 0; j < kVarSlots; ++j) asm volatile("" : "+v"(t.va[j]), "+v"(t.vb[j]));
+#if BP_VA_FULL
+#pragma unroll
+  for (int j = 0; j < kVarSlots; ++j) asm volatile("" : "+v"(t.va1[j]));
+#endif
 #pragma unroll
   for (int k = 0; k < kChkSlots; ++k)
 #pragma unroll
@@ -582,7 +602,11 @@ __global__ __launch_bounds__(kWave, BP_WAVES_PER_EU) void k_bp(BpArgs a) {
       // (A) hard decision + variable -> check arguments
 #pragma unroll
       for (int j = 0; j < kVarSlots; ++j) {
+#if BP_VA_FULL
+        const uint32_t a0 = tb.va[j], a1 = tb.va1[j], a2 = tb.vb[j];
+#else
         const uint32_t a0 = tb.va[j] & 0xFFFFu, a1 = tb.va[j] >> 16, a2 = tb.vb[j];
+#endif
         const double t0 = *(lds_f64*)(uintptr_t)a0;
         const double t1 = *(lds_f64*)(uintptr_t)a1;
         const double t2 = *(lds_f64*)(uintptr_t)a2;
