@@ -84,6 +84,22 @@ def sync_select(wf, max_candidates, min_score, want_grid=False, flags=0):
     return cands, g, int(warn.item())
 
 
+def sync_scores(wf, cand_list):
+    """ft8_sync_score of arbitrary (abs_time, abs_freq) pairs (k_score_list) -> (scores in the
+    waterfall dtype, IndexError flags)."""
+    torch = _lib.require_gpu()
+    ctx = _lib.context()
+    d, f64, T, F = waterfall_to_device(wf)
+    n = len(cand_list)
+    c = torch.tensor([[int(a), int(b)] for a, b in cand_list] or [[0, 0]], dtype=torch.int32, device=d.device)
+    out = torch.empty(max(n, 1), dtype=d.dtype, device=d.device)
+    err = torch.zeros(max(n, 1), dtype=torch.int32, device=d.device)
+    rc = _lib.lib().ft8_sync_score(ctx.handle, _lib.ptr(d), int(f64), T, F, int(wf.time_osr), int(wf.freq_osr),
+                                   _lib.ptr(c), n, _lib.ptr(out), _lib.ptr(err), _lib.stream_handle())
+    ctx.check(rc, "ft8_sync_score")
+    return out.cpu().numpy()[:n], err.cpu().numpy()[:n].astype(bool)
+
+
 def llr(wf, cand_list, normalize):
     """cand_list [(abs_time, abs_freq)] -> LLRs [n, 174] (float64)."""
     torch = _lib.require_gpu()

@@ -885,6 +885,16 @@ int ft8_sync_select(ft8_ctx* c, const void* d_wf, int wf_f64, int32_t n_slots, i
                         (hipStream_t)stream);
 }
 
+int ft8_sync_score(ft8_ctx* c, const void* d_wf, int wf_f64, int32_t T, int32_t F, int32_t sps, int32_t bpt,
+                   const int32_t* d_cand, int32_t n, void* d_out, int32_t* d_err, void* stream) {
+  if (c) c->replay_ok = false;
+  if (!c || n < 0 || (n > 0 && (!d_wf || !d_cand || !d_out || !d_err))) return fail(c, FT8_E_ARG, "bad argument");
+  if (T <= 0 || F <= 0 || sps <= 0 || bpt <= 0) return fail(c, FT8_E_ARG, "empty waterfall or bad oversampling");
+  DeviceGuard dg(c->device);
+  hipError_t e = launch_score_list(d_wf, wf_f64, T, F, sps, bpt, d_cand, n, d_out, d_err, (hipStream_t)stream);
+  return e == hipSuccess ? FT8_OK : hipfail(c, e, "score launch");
+}
+
 int ft8_llr(ft8_ctx* c, const void* d_wf, int wf_f64, int32_t T, int32_t F, int32_t sps, int32_t bpt,
             const int32_t* d_cand, int32_t n, int normalize, double* d_llr, void* stream) {
   if (c) c->replay_ok = false;

@@ -108,6 +108,9 @@ struct TieArgs {
 hipError_t launch_tie_apply(const TieArgs& a, int32_t* cand, double* cand_score, hipStream_t s);
 hipError_t launch_score(const SyncLaunch& a, hipStream_t s);
 hipError_t launch_select(const SyncLaunch& a, hipStream_t s);
+// ft8_sync_score for arbitrary candidates [n][2] = (abs_time, abs_freq); err[i] = 1: IndexError
+hipError_t launch_score_list(const void* wf, int wf_f64, int T, int F, int sps, int bpt, const int32_t* cand,
+                             int n, void* out, int32_t* err, hipStream_t s);
 
 // ---- LLR + BP + CRC ------------------------------------------------------------------------
 struct BpLaunch {

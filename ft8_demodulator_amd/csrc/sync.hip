@@ -125,6 +125,47 @@ __global__ __launch_bounds__(kScoreThreads) void k_score(ScoreArgs a) {
   }
 }
 
+// ---- k_score_list: ft8_sync_score for arbitrary candidates ------------------------------------------
+// One thread per (abs_time, abs_freq), exactly ft8_sync_score (ft8_decode.py:47-100) including what
+// the grid kernels never meet: FT8Candidate.get_log_power indexes mag[freq, time] with NumPy's rules
+// (ftx_types.py:45-47), so a negative index counts from the end and an index past either end raises
+// IndexError -- flagged in err[i] (the score is then meaningless).  Only the time-block test of the
+// reference guards the accesses; nothing guards the frequency.
+template <typename T>
+__global__ void k_score_list(const T* wf, int Tn, int F, int sps, int bpt, const int32_t* cand, int n, T* out,
+                             int32_t* err) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int at = cand[2 * i], af = cand[2 * i + 1];
+  const int nb = Tn / sps;
+  bool bad = false;
+  auto get = [&](int64_t t, int64_t f) -> T {  // mag[f, t] with NumPy indexing
+    if (f < 0) f += F;
+    if (t < 0) t += Tn;
+    if (f < 0 || f >= F || t < 0 || t >= Tn) { bad = true; return (T)0; }
+    return wf[t * F + f];
+  };
+  const int base = floordiv(at, sps);
+  T score = (T)0;
+  int cnt = 0;
+  for (int m = 0; m < 3; ++m) {
+    for (int k = 0; k < 7; ++k) {
+      const int block = 36 * m + k;
+      const int ba = base + block;
+      if (ba < 0 || ba >= nb) continue;
+      const int tone = kCostasD[k];
+      const int64_t row = (int64_t)at + (int64_t)block * sps, col = (int64_t)af + (int64_t)tone * bpt;
+      const T p = get(row, col);
+      if (tone > 0) { score += (T)(p - get(row, col - bpt)); cnt++; }
+      if (tone < 7) { score += (T)(p - get(row, col + bpt)); cnt++; }
+      if (k > 0 && ba > 0) { score += (T)(p - get(row - sps, col)); cnt++; }
+      if (k < 6 && ba + 1 < nb) { score += (T)(p - get(row + sps, col)); cnt++; }
+    }
+  }
+  out[i] = (cnt == 0 || isnan(score) || isinf(score)) ? (T)-INFINITY : score / (T)cnt;
+  err[i] = bad ? 1 : 0;
+}
+
 // ---- k_score2 ----------------------------------------------------------------------------------
 constexpr int kS2TW = 128;                 // grid columns per workgroup (64 lanes x 2)
 constexpr int kS2R = 22;                   // grid rows per workgroup (88 = 4 x 22 at 12 kHz)
@@ -901,6 +942,19 @@ hipError_t launch_score(const SyncLaunch& L, hipStream_t s) {
   if (L.NT <= 0 || L.NF <= 0 || L.n_slots <= 0) return hipSuccess;
   if (L.wf_f64) return launch_score_t<double, 32>(L, s);
   return launch_score_t<float, 64>(L, s);
+}
+
+hipError_t launch_score_list(const void* wf, int wf_f64, int T, int F, int sps, int bpt, const int32_t* cand,
+                             int n, void* out, int32_t* err, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  const unsigned blocks = (unsigned)((n + 255) / 256);
+  if (wf_f64)
+    hipLaunchKernelGGL(k_score_list<double>, dim3(blocks), dim3(256), 0, s, (const double*)wf, T, F, sps, bpt, cand,
+                       n, (double*)out, err);
+  else
+    hipLaunchKernelGGL(k_score_list<float>, dim3(blocks), dim3(256), 0, s, (const float*)wf, T, F, sps, bpt, cand, n,
+                       (float*)out, err);
+  return hipGetLastError();
 }
 
 hipError_t launch_select(const SyncLaunch& L, hipStream_t s) {

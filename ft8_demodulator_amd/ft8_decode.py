@@ -11,7 +11,9 @@ Deliberate differences (DESIGN.md "Parity"):
     raises IndexError at ft8_decode.py:346; its own test expects []);
   * exact score ties that reach a heap comparison are ordered by scan position (the reference
     raises TypeError, FT8Candidate being unordered);
-  * the reference's progress prints are behind verbose=True.
+  * the reference's progress prints are behind verbose=True;
+  * max_candidates is capped at 4096 (ft8_limits(); the selection holds its candidates in LDS):
+    a larger value raises Ft8Error (FT8_E_RANGE) instead of running -- the reference has no cap.
 """
 from __future__ import annotations
 
@@ -37,15 +39,25 @@ FT8_Costas_pattern = [3, 1, 4, 0, 6, 5, 2]
 
 
 def ft8_sync_score(wf: FT8Waterfall, candidate: FT8Candidate) -> float:
-    """ft8_decode.py:47-100 for a candidate on the ft8_find_candidates grid."""
-    sps, bpt = wf.time_osr, wf.freq_osr
-    F, T = wf.mag.shape
-    t0, NT, NF = _device.grid_shape(T, F, sps, bpt)
-    i, j = candidate.abs_time - t0, candidate.abs_freq
-    if not (0 <= i < NT and 0 <= j < NF):
-        raise ValueError("candidate outside the ft8_find_candidates search grid")
-    _, grid, _ = _device.sync_select(wf, 0, 0, want_grid=True)
-    return grid[i, j]
+    """ft8_decode.py:47-100 for any candidate, on or off the search grid (one GPU thread,
+    k_score_list): -inf (a Python float) when nothing is comparable, else the waterfall-dtype mean;
+    IndexError where the reference's get_log_power (ftx_types.py:45-47) would index past the
+    waterfall (negative indices count from the end, as NumPy's do)."""
+    s, err = _device.sync_scores(wf, [(candidate.abs_time, candidate.abs_freq)])
+    if err[0]:
+        raise IndexError("index out of bounds for the waterfall (FT8Candidate.get_log_power)")
+    v = s[0]
+    return float("-inf") if v == -np.inf else v
+
+
+def ft8_sync_scores(wf: FT8Waterfall, candidates) -> np.ndarray:
+    """Vectorised ft8_sync_score over [(abs_time, abs_freq), ...] (build-defined helper, one launch);
+    IndexError if any candidate would raise it."""
+    s, err = _device.sync_scores(wf, [(c.abs_time, c.abs_freq) if isinstance(c, FT8Candidate) else tuple(c)
+                                      for c in candidates])
+    if err.any():
+        raise IndexError(f"candidate {int(np.argmax(err))}: index out of bounds for the waterfall")
+    return s
 
 
 def ft8_score_grid(wf: FT8Waterfall) -> np.ndarray:

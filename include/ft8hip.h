@@ -142,6 +142,15 @@ int ft8_sync_select(ft8_ctx* ctx, const void* d_wf, int wf_f64, int32_t n_slots,
                     int32_t F, const ft8_params* p, int32_t* d_cand, double* d_cand_score,
                     int32_t* d_cand_count, void* d_scores, void* stream);
 
+/* ft8_sync_score itself (ft8_decode.py:47-100) for arbitrary candidates d_cand[n][2] = (abs_time,
+ * abs_freq), on or off the search grid: d_out[n] in the waterfall dtype (-inf as the reference
+ * returns it), d_err[n] = 1 where the reference's get_log_power (ftx_types.py:45-47) would raise
+ * IndexError (NumPy indexing: negative indices count from the end, nothing guards the frequency
+ * axis).  d_wf as for ft8_sync_select. */
+int ft8_sync_score(ft8_ctx* ctx, const void* d_wf, int wf_f64, int32_t T, int32_t F, int32_t steps_per_symbol,
+                   int32_t bins_per_tone, const int32_t* d_cand, int32_t n, void* d_out, int32_t* d_err,
+                   void* stream);
+
 /* ---- stage 3: soft LLRs --------------------------------------------------------------------
  * Replaces ft8_extract_likelihood + ftx_normalize_logl (ft8_decode.py:151-198).  d_cand[n][3] =
  * (slot, abs_time, abs_freq).  Output d_llr[n][174] (double). */

@@ -232,3 +232,48 @@ def test_selection_with_ties_vs_oracle(gpu, oracle):
             assert bool(warn & 1) == tie, (trial, N, ms)
             cases += bool(warn & 4)
     assert cases >= 10   # the replay path ran
+
+
+def test_sync_score_any_candidate_matches_reference(golden, gpu):
+    """ft8_sync_score off the search grid (k_score_list): NumPy wrap-around of negative frequency
+    indices, IndexError past the last bin, -inf when no block is comparable -- against the
+    reference's own values (tests/golden/syncscore.json, tools/make_golden_syncscore.py)."""
+    import json
+    import os
+    from conftest import GOLD
+    from ft8_demodulator_amd import FT8Candidate, FT8Waterfall, ft8_sync_score
+    _, arr = golden
+    with open(os.path.join(GOLD, "syncscore.json")) as f:
+        cases = json.load(f)
+    for c in cases:
+        mag = arr[f"sync_{c['case']}_mag"]
+        wf = FT8Waterfall(mag=mag, time_osr=c["sps"], freq_osr=c["bpt"])
+        cand = FT8Candidate(waterfall=wf, abs_time=c["abs_time"], abs_freq=c["abs_freq"])
+        if c["error"]:
+            with pytest.raises(IndexError):
+                ft8_sync_score(wf, cand)
+            continue
+        v = ft8_sync_score(wf, cand)
+        assert type(v).__name__ == c["dtype"], c
+        assert float(v) == c["score"], c   # bit-exact (float32 widened exactly / float64)
+    # on the grid it equals the grid kernel
+    from ft8_demodulator_amd import ft8_score_grid
+    from ft8_demodulator_amd.ft8_decode import ft8_sync_scores
+    wf = FT8Waterfall(mag=arr["sync_rand32_mag"], time_osr=2, freq_osr=2)
+    g = ft8_score_grid(wf)
+    pts = [(-20 + i, j) for i in (0, 5, 37, g.shape[0] - 1) for j in (0, 1, 40, g.shape[1] - 1)]
+    s = ft8_sync_scores(wf, pts)
+    assert np.array_equal(s, np.array([g[t + 20, f] for t, f in pts], dtype=s.dtype))
+
+
+def test_max_candidates_limit_is_an_error(gpu):
+    """Deliberate deviation: the selection holds its candidates in LDS, so
+    max_candidates above ft8_limits() (4096) is refused with FT8_E_RANGE rather than silently
+    truncated; the reference has no cap (ft8_decode.py:102-149)."""
+    from ft8_demodulator_amd import _lib, decode_ft8_message
+    lim = _lib.limits()["max_candidates"]
+    assert lim == 4096
+    x = np.random.default_rng(1).standard_normal(180000).astype(np.float32)
+    assert decode_ft8_message(x, 12000, max_candidates=lim, min_score=100) == []
+    with pytest.raises(_lib.Ft8Error, match="max_candidates"):
+        decode_ft8_message(x, 12000, max_candidates=lim + 1, min_score=100)
