@@ -13,7 +13,7 @@ Deliberate differences (DESIGN.md "Parity"):
     raises TypeError, FT8Candidate being unordered);
   * the reference's progress prints are behind verbose=True;
   * max_candidates is capped at 4096 (ft8_limits(); the selection holds its candidates in LDS):
-    a larger value raises Ft8Error (FT8_E_RANGE) instead of running -- the reference has no cap.
+    a larger value raises ValueError (FT8_E_RANGE) instead of running -- the reference has no cap.
 """
 from __future__ import annotations
 

@@ -268,12 +268,12 @@ def test_sync_score_any_candidate_matches_reference(golden, gpu):
 
 def test_max_candidates_limit_is_an_error(gpu):
     """Deliberate deviation: the selection holds its candidates in LDS, so
-    max_candidates above ft8_limits() (4096) is refused with FT8_E_RANGE rather than silently
+    max_candidates above ft8_limits() (4096) is refused with FT8_E_RANGE (ValueError) rather than silently
     truncated; the reference has no cap (ft8_decode.py:102-149)."""
     from ft8_demodulator_amd import _lib, decode_ft8_message
     lim = _lib.limits()["max_candidates"]
     assert lim == 4096
     x = np.random.default_rng(1).standard_normal(180000).astype(np.float32)
     assert decode_ft8_message(x, 12000, max_candidates=lim, min_score=100) == []
-    with pytest.raises(_lib.Ft8Error, match="max_candidates"):
+    with pytest.raises(ValueError, match="max_candidates"):
         decode_ft8_message(x, 12000, max_candidates=lim + 1, min_score=100)
