@@ -568,8 +568,10 @@ def main():
     # and WRITE_SIZE passes of the same 256-slot workload), or null when it is absent
     import glob
     traffic, tsrc = {}, None
-    tfiles = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")),
-                    key=lambda p_: int(os.path.basename(p_)[1:].split("_")[0]))
+    def _rv(p_):  # rNN[_vK]_pmc_traffic.json -> (NN, K)
+        parts = os.path.basename(p_)[1:].split("_")
+        return int(parts[0]), int(parts[1][1:]) if parts[1].startswith("v") and parts[1][1:].isdigit() else -1
+    tfiles = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")), key=_rv)
     if tfiles:
         tsrc = os.path.relpath(tfiles[-1], ROOT)
         with open(tfiles[-1]) as f:

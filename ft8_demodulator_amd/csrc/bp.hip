@@ -336,11 +336,12 @@ __device__ bool tie_order(const TieArgs& a, int slot) {
   int32_t* mp = t + 4 * N;
   int32_t* mk = t + 5 * N;
   const int rec = t[7 * N];
-  const float* sc = a.scores + (int64_t)slot * a.score_stride;
+  const float* psc = reinterpret_cast<const float*>(t + 7 * N + 2);  // scores in push order
+  const double* ssc = a.cand_score + (int64_t)slot * N;              // scores in select order
   unsigned hh[kReplayRegs], hl[kReplayRegs];
-  heap_load(sc, push, nsel, hh, hl);
+  heap_load(psc, push, nsel, hh, hl);
   int tie = heap_pushes(nsel, hh, hl);
-  if (rec >= 0) tie |= heap_record(nsel, hh, hl, mono_neg(sc[rec]), (unsigned)rec);
+  if (rec >= 0) tie |= heap_record(nsel, hh, hl, mono_neg(__int_as_float(t[7 * N + 1])), (unsigned)rec);
 
   // members: select ranks whose score equals a neighbour's; record each one's heap position
   int M = 0;
@@ -350,8 +351,8 @@ __device__ bool tie_order(const TieArgs& a, int slot) {
     bool mem = false;
     if (i < nsel) {
       idx = (unsigned)sel[i];
-      key = mono_neg(sc[idx]);
-      mem = (i > 0 && mono_neg(sc[sel[i - 1]]) == key) || (i + 1 < nsel && mono_neg(sc[sel[i + 1]]) == key);
+      key = mono_neg((float)ssc[i]);
+      mem = (i > 0 && mono_neg((float)ssc[i - 1]) == key) || (i + 1 < nsel && mono_neg((float)ssc[i + 1]) == key);
     }
     unsigned long long b = __ballot(mem);
     while (b) {
@@ -865,7 +866,7 @@ BpArgs make_args(const BpLaunch& L) {
   a.work = L.work;
   a.stats = L.stats;
   a.slot0 = L.slot0;
-  a.tie = TieArgs{L.n_slots, L.N, L.cand_count, L.warn, L.tie, L.tie_scores, L.tie_score_stride};
+  a.tie = TieArgs{L.n_slots, L.N, L.cand_count, L.warn, L.tie, L.cand_score};
   a.tie_blocks = (L.tie && L.mode == 0) ? (L.n_slots + 7) / 8 * 8 : 0;
   return a;
 }

@@ -54,7 +54,7 @@ struct ft8_ctx {
   std::string err;
   std::vector<PlanEntry> plans;
   std::vector<WinEntry> wins;
-  DevBuf wf, scores, cand, cand_score, cand_count, warn, rowsum, res_all, work, stats, llr, tie;
+  DevBuf wf, scores, smask, cand, cand_score, cand_count, warn, rowsum, res_all, work, stats, llr, tie;
   // FT8_FLAG_SUBTRACT: residual samples, per-record fits, pass-1 / pass-2 records
   DevBuf residual, sub_est, out1, counts1, out2, counts2;
   // cumulative GFSK pulse of the transmit chain for one nsps (double and float)
@@ -388,6 +388,10 @@ Grid grid_of(int T, int F, int sps, int bpt) {
   g.NF = F - 7 * bpt > 0 ? F - 7 * bpt : 0;
   return g;
 }
+// score scratch per slot: elements (the full grid NT x NF, or the compact layout NT x nseg x 128)
+// and segment-mask words
+size_t score_elems(const Grid& g) { return (size_t)g.NT * n_segments(g.NF) * kSegCols; }
+size_t smask_words(const Grid& g) { return (size_t)g.NT * n_segments(g.NF) * 2; }
 
 int decode_pass(ft8_ctx* c, const void* d_samples, int dtype, int64_t n_samples, int32_t n_slots,
                 int64_t slot_stride, const ft8_params* p, ft8_result* d_out, int32_t* d_counts, int32_t cap,
@@ -397,8 +401,8 @@ int subtract_core(ft8_ctx* c, const void* x, int dtype, float* resid, int64_t n_
                   const int32_t* counts, int cap, hipStream_t s);
 int gfsk_tables(ft8_ctx* c, int nsps);
 int sync_select_core(ft8_ctx* c, const void* d_wf, int wf_f64, int n_slots, int T, int F, const ft8_params* p,
-                     int32_t* cand, double* cand_score, int32_t* cand_count, void* scores,
-                     int32_t* warn, RowSummary* rowsum, hipStream_t s, int32_t* tie = nullptr);
+                     int32_t* cand, double* cand_score, int32_t* cand_count, void* scores, uint64_t* smask,
+                     int compact, int32_t* warn, RowSummary* rowsum, hipStream_t s, int32_t* tie = nullptr);
 
 int do_sync_select(ft8_ctx* c, const void* d_wf, int wf_f64, int n_slots, int T, int F, const ft8_params* p,
                    int32_t* cand, double* cand_score, int32_t* cand_count, void* d_scores, hipStream_t s) {
@@ -414,11 +418,13 @@ int do_sync_select(ft8_ctx* c, const void* d_wf, int wf_f64, int n_slots, int T,
   }
   const size_t esz = wf_f64 ? 8 : 4;
   int rc;
+  // without a caller grid the scores stay in the compact layout (only passing scores written)
   void* scores = d_scores;
   if (!scores) {
-    if ((rc = ensure(c, c->scores, esz * (size_t)n_slots * g.NT * g.NF))) return rc;
+    if ((rc = ensure(c, c->scores, esz * (size_t)n_slots * score_elems(g)))) return rc;
     scores = c->scores.p;
   }
+  if ((rc = ensure(c, c->smask, sizeof(uint64_t) * (size_t)n_slots * smask_words(g)))) return rc;
   if ((rc = ensure(c, c->warn, sizeof(int32_t) * (size_t)n_slots))) return rc;
   if ((rc = ensure(c, c->rowsum, sizeof(RowSummary) * (size_t)n_slots * g.NT))) return rc;
   // float32 scores: k_select leaves equal scores in scan order and k_tie_apply replays the
@@ -429,22 +435,23 @@ int do_sync_select(ft8_ctx* c, const void* d_wf, int wf_f64, int n_slots, int T,
     tie = (int32_t*)c->tie.p;
   }
   int32_t* warn = (int32_t*)c->warn.p;
-  if ((rc = sync_select_core(c, d_wf, wf_f64, n_slots, T, F, p, cand, cand_score, cand_count, scores, warn,
-                             (RowSummary*)c->rowsum.p, s, tie)))
+  if ((rc = sync_select_core(c, d_wf, wf_f64, n_slots, T, F, p, cand, cand_score, cand_count, scores,
+                             (uint64_t*)c->smask.p, d_scores == nullptr, warn, (RowSummary*)c->rowsum.p, s, tie)))
     return rc;
   if (tie) {
-    const TieArgs ta{n_slots, N, cand_count, warn, tie, (const float*)scores, (int64_t)g.NT * g.NF};
+    const TieArgs ta{n_slots, N, cand_count, warn, tie, cand_score};
     hipError_t e = launch_tie_apply(ta, cand, cand_score, s);
     if (e != hipSuccess) return hipfail(c, e, "tie launch");
   }
   return FT8_OK;
 }
 
-// score + select on caller-provided scratch (scores [n_slots][NT][NF], warn [n_slots],
-// rowsum [n_slots][NT])
+// score + select on caller-provided scratch (scores [n_slots][score_elems], smask
+// [n_slots][smask_words], warn [n_slots], rowsum [n_slots][NT]); compact: the score kernel may
+// write only the passing scores (k_score2 path, reference selection), else the full grid
 int sync_select_core(ft8_ctx* c, const void* d_wf, int wf_f64, int n_slots, int T, int F, const ft8_params* p,
-                     int32_t* cand, double* cand_score, int32_t* cand_count, void* scores,
-                     int32_t* warn, RowSummary* rowsum, hipStream_t s, int32_t* tie) {
+                     int32_t* cand, double* cand_score, int32_t* cand_count, void* scores, uint64_t* smask,
+                     int compact, int32_t* warn, RowSummary* rowsum, hipStream_t s, int32_t* tie) {
   const int N = p->max_candidates;
   Grid g = grid_of(T, F, p->steps_per_symbol, p->bins_per_tone);
   SyncLaunch L{};
@@ -459,6 +466,8 @@ int sync_select_core(ft8_ctx* c, const void* d_wf, int wf_f64, int n_slots, int 
   L.NT = g.NT;
   L.NF = g.NF;
   L.scores = scores;
+  L.smask = smask;
+  L.compact = compact;
   L.N = N;
   L.min_score = p->min_score;
   L.min_score_f64 = p->min_score_f64;
@@ -529,7 +538,8 @@ int decode_pass(ft8_ctx* c, const void* d_samples, int dtype, int64_t n_samples,
     int32_t* tie = f64 ? nullptr : (int32_t*)c->tie.p + (size_t)c0 * tie_stride(N);
     int32_t* warn = (int32_t*)c->warn.p + c0;
     if ((rc = sync_select_core(c, wf, f64, ns, T, F, p, cand, cand_score, cand_count,
-                               (char*)c->scores.p + esz * (size_t)c0 * gr.NT * gr.NF, (int32_t*)c->warn.p + c0,
+                               (char*)c->scores.p + esz * (size_t)c0 * score_elems(gr),
+                               (uint64_t*)c->smask.p + (size_t)c0 * smask_words(gr), 1, (int32_t*)c->warn.p + c0,
                                (RowSummary*)c->rowsum.p + (size_t)c0 * gr.NT, cs, tie)))
       return rc;
     BpLaunch B{};
@@ -557,8 +567,6 @@ int decode_pass(ft8_ctx* c, const void* d_samples, int dtype, int64_t n_samples,
     B.grid_waves = n_str > 0 ? c->bp_waves : 8;  // clamped to the kernel's BP_WAVES_PER_EU
     B.tie = tie;
     B.warn = warn;
-    B.tie_scores = (const float*)((char*)c->scores.p + esz * (size_t)c0 * gr.NT * gr.NF);
-    B.tie_score_stride = (int64_t)gr.NT * gr.NF;
     StageTimer t6(c, 6, cs);
     e = launch_llr(B, cs);
     t6.done();
@@ -828,7 +836,7 @@ int ft8_destroy(ft8_ctx* c) {
   if (!c) return FT8_OK;
   {
     DeviceGuard dg(c->device);
-    for (auto* b : {&c->wf, &c->scores, &c->cand, &c->cand_score, &c->cand_count, &c->warn, &c->rowsum,
+    for (auto* b : {&c->wf, &c->scores, &c->smask, &c->cand, &c->cand_score, &c->cand_count, &c->warn, &c->rowsum,
                     &c->res_all, &c->work, &c->stats, &c->llr, &c->tie, &c->residual, &c->sub_est, &c->out1,
                     &c->counts1, &c->out2, &c->counts2, &c->gfsk_P, &c->gfsk_Pf, &c->drift_idx, &c->drift_tmpl})
       if (b->p) (void)hipFree(b->p);
@@ -996,7 +1004,8 @@ int ft8_decode_batch(ft8_ctx* c, const void* d_samples, int dtype, int64_t n_sam
   if ((rc = ensure(c, c->cand_count, sizeof(int32_t) * (size_t)n_slots))) return rc;
   if ((rc = ensure(c, c->res_all, sizeof(ft8_result) * (size_t)n_slots * N))) return rc;
   if ((rc = ensure(c, c->llr, sizeof(double) * FT8_LDPC_N * (size_t)n_slots * N))) return rc;
-  if ((rc = ensure(c, c->scores, esz * (size_t)n_slots * gr.NT * gr.NF))) return rc;
+  if ((rc = ensure(c, c->scores, esz * (size_t)n_slots * score_elems(gr)))) return rc;
+  if ((rc = ensure(c, c->smask, sizeof(uint64_t) * (size_t)n_slots * smask_words(gr)))) return rc;
   if ((rc = ensure(c, c->warn, sizeof(int32_t) * (size_t)n_slots))) return rc;
   if ((rc = ensure(c, c->rowsum, sizeof(RowSummary) * (size_t)n_slots * gr.NT))) return rc;
   if (!f64 && (rc = ensure(c, c->tie, sizeof(int32_t) * (size_t)n_slots * tie_stride(N)))) return rc;

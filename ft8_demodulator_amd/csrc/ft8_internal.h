@@ -77,7 +77,11 @@ struct SyncLaunch {
   int n_slots, T, F;
   int sps, bpt;
   int t0, NT, NF;          // abs_time grid = [t0, t0+NT), abs_freq grid = [0, NF)
-  void* scores;            // [n_slots][NT][NF] in wf dtype
+  void* scores;            // full grid [n_slots][NT][NF] in wf dtype, or (compact) the passing
+                           // scores of every segment packed at its start [n_slots][NT][nseg][128]
+  uint64_t* smask;         // [n_slots][NT][nseg][2]: passing columns of each 128-column segment
+                           // (word 0: even columns 2l -> bit l, word 1: odd columns 2l + 1)
+  int compact = 0;         // request the compact score layout (honoured by the k_score2 path)
   int N;                   // max candidates
   double min_score;
   int min_score_f64;
@@ -94,19 +98,24 @@ struct SyncLaunch {
 };
 
 // deferred tie order, per slot: push order [N] | select order [N] | final order [N] |
-// scratch [4N] | last record [1] (heap_replay.h)
-inline __host__ __device__ int64_t tie_stride(int N) { return 7 * (int64_t)N + 2; }
+// scratch [4N] | last record [1] | its score [1] (float bits) | scores in push order [N]
+// (heap_replay.h)
+inline __host__ __device__ int64_t tie_stride(int N) { return 8 * (int64_t)N + 2; }
 struct TieArgs {
   int n_slots, N;
   const int32_t* cand_count;
   int32_t* warn;           // bit 3 set by k_select: replay this slot's heap; bit 0 set on a tie
   int32_t* tie;            // [n_slots][tie_stride(N)]
-  const float* scores;     // float32 score grid [n_slots][score_stride]
-  int64_t score_stride;
+  const double* cand_score;  // [n_slots][N] selected scores in select order (float32 values)
 };
 // the deferred order applied to a candidate list ([n_slots][N][2] + [n_slots][N])
 hipError_t launch_tie_apply(const TieArgs& a, int32_t* cand, double* cand_score, hipStream_t s);
 hipError_t launch_score(const SyncLaunch& a, hipStream_t s);
+// score segments: 128 grid columns of one row; the compact layout holds only passing scores
+constexpr int kSegCols = 128;
+inline __host__ __device__ int n_segments(int NF) { return (NF + kSegCols - 1) / kSegCols; }
+// whether launch_score writes the compact layout for this launch (else the full grid)
+bool score_compact(const SyncLaunch& a);
 hipError_t launch_select(const SyncLaunch& a, hipStream_t s);
 // ft8_sync_score for arbitrary candidates [n][2] = (abs_time, abs_freq); err[i] = 1: IndexError
 hipError_t launch_score_list(const void* wf, int wf_f64, int T, int F, int sps, int bpt, const int32_t* cand,
@@ -139,8 +148,6 @@ struct BpLaunch {
   // replayed by k_llr's first workgroups
   int32_t* tie = nullptr;  // [n_slots][tie_stride(N)]
   int32_t* warn = nullptr; // [n_slots]
-  const float* tie_scores = nullptr;  // float32 score grid [n_slots][tie_score_stride]
-  int64_t tie_score_stride = 0;
 };
 hipError_t launch_llr(const BpLaunch& a, hipStream_t s);  // k_llr: waterfall -> LLRs
 hipError_t launch_bp(const BpLaunch& a, hipStream_t s);   // k_bp: LLRs -> BP + CRC

@@ -66,9 +66,9 @@ __device__ inline void heap_set(unsigned (&hh)[kReplayRegs], unsigned (&hl)[kRep
 }
 
 // Items in push order: lane l of register k gets push n = 64k + l - 1 (heap position 64k + l),
-// scan index push[n], score sc[push[n]].  nsel <= kReplayMax.
+// scan index push[n], score psc[n].  nsel <= kReplayMax.
 template <typename IdxPtr>
-__device__ inline void heap_load(const float* sc, IdxPtr push, int nsel, unsigned (&hh)[kReplayRegs],
+__device__ inline void heap_load(const float* psc, IdxPtr push, int nsel, unsigned (&hh)[kReplayRegs],
                                  unsigned (&hl)[kReplayRegs]) {
   const int lane = threadIdx.x & 63;
 #pragma unroll
@@ -77,7 +77,7 @@ __device__ inline void heap_load(const float* sc, IdxPtr push, int nsel, unsigne
     unsigned h = 0, l = 0;
     if (n >= 0 && n < nsel) {
       const int idx = push[n];
-      h = mono_neg(sc[idx]);
+      h = mono_neg(psc[n]);
       l = (unsigned)idx;
     }
     hh[k] = h;

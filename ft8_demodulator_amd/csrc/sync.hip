@@ -49,6 +49,8 @@ struct ScoreArgs {
   int t0, NT, NF;
   int rlo, nrows;    // staged rows [rlo, rlo + nrows)
   void* scores;
+  uint64_t* smask;   // [slot][NT][nseg][2] passing columns per 128-column segment
+  int nseg;
   RowSummary* rowsum;
   double min_score;
   int cmp_f64;
@@ -121,6 +123,10 @@ __global__ __launch_bounds__(kScoreThreads) void k_score(ScoreArgs a) {
     if (passes(res, a.min_score, a.cmp_f64)) {
       atomicAdd(&rs[ti].count, 1u);
       atomicMax(&rs[ti].maxkey, order_key((double)res));
+      const int c = af % kSegCols;
+      atomicOr(reinterpret_cast<unsigned long long*>(
+                   &a.smask[(((int64_t)slot * a.NT + ti) * a.nseg + af / kSegCols) * 2 + (c & 1)]),
+               1ull << (c >> 1));
     }
   }
 }
@@ -167,11 +173,44 @@ __global__ void k_score_list(const T* wf, int Tn, int F, int sps, int bpt, const
 }
 
 // ---- k_score2 ----------------------------------------------------------------------------------
+#ifndef S2_LOADFIRST
+#define S2_LOADFIRST 0
+#endif
 constexpr int kS2TW = 128;                 // grid columns per workgroup (64 lanes x 2)
 constexpr int kS2R = 22;                   // grid rows per workgroup (88 = 4 x 22 at 12 kHz)
 constexpr int kS2Waves = 11;               // each wave takes rows w, w + 11
 constexpr int kS2Threads = kS2Waves * kWave;
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// The 25 differences of a Costas band in the reference order (ft8_decode.py:66-94: per symbol k,
+// tone-1, tone+1, time-1, time+1), as slots of a list of distinct (row, column) reads relative to
+// the band's first staged row (rows in steps_per_symbol, columns in bins_per_tone)
+struct BandPlan {
+  int nload;
+  int row[32], col[32];
+  int ctr[25], nbr[25];
+};
+constexpr BandPlan band_plan() {
+  BandPlan b{};
+  auto slot = [&b](int r, int c) {
+    for (int i = 0; i < b.nload; ++i)
+      if (b.row[i] == r && b.col[i] == c) return i;
+    b.row[b.nload] = r;
+    b.col[b.nload] = c;
+    return b.nload++;
+  };
+  int t = 0;
+  for (int k = 0; k < 7; ++k) {
+    const int tone = kCostasC[k], r = k + 1;
+    const int c = slot(r, tone);
+    if (tone > 0) { b.ctr[t] = c; b.nbr[t++] = slot(r, tone - 1); }
+    if (tone < 7) { b.ctr[t] = c; b.nbr[t++] = slot(r, tone + 1); }
+    if (k > 0) { b.ctr[t] = c; b.nbr[t++] = slot(r - 1, tone); }
+    if (k < 6) { b.ctr[t] = c; b.nbr[t++] = slot(r + 1, tone); }
+  }
+  return b;
+}
+static_assert(band_plan().nload == 30, "Costas band reads");
 
 template <int BPT, int SPS>
 struct S2Geom {
@@ -179,6 +218,28 @@ struct S2Geom {
   static constexpr int H = kS2R + 8 * SPS;               // staged rows per Costas band
   static constexpr int kFloats = 3 * H * P;
 };
+
+// maximum over the wave (no NaN), on order-preserving integer keys (a float max would re-quiet
+// every DPP operand): rotations inside each 16-lane row (DPP row_ror 8, 4, 2, 1), then the four
+// row maxima in scalar registers -- instead of six ds_bpermute rounds
+__device__ __forceinline__ int fkey(float v) {
+  const int i = __float_as_int(v);
+  return i ^ ((i >> 31) & 0x7fffffff);
+}
+template <int CTRL>
+__device__ __forceinline__ int dpp_max(int k) {
+  return max(k, __builtin_amdgcn_mov_dpp(k, CTRL, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float wave_max(float v) {
+  int k = fkey(v);
+  k = dpp_max<0x128>(k);  // row_ror:8
+  k = dpp_max<0x124>(k);  // row_ror:4
+  k = dpp_max<0x122>(k);  // row_ror:2
+  k = dpp_max<0x121>(k);  // row_ror:1
+  const int m = max(max(__builtin_amdgcn_readlane(k, 0), __builtin_amdgcn_readlane(k, 16)),
+                    max(__builtin_amdgcn_readlane(k, 32), __builtin_amdgcn_readlane(k, 48)));
+  return __int_as_float(m ^ ((m >> 31) & 0x7fffffff));
+}
 
 // volatile LDS load: one ds_read_b64 per pair.  The compiler would otherwise merge neighbouring
 // pairs into ds_read2_b64, which moves half as many bytes per LDS cycle (measured: k_score2 0.27
@@ -189,8 +250,9 @@ __device__ __forceinline__ f32x2 ld2(const float* p) {
   else return f32x2{p[0], p[1]};
 }
 
-template <int BPT, int SPS>
+template <int BPT, int SPS, bool COMPACT>
 __global__ __launch_bounds__(kS2Threads) void k_score2(ScoreArgs a) {
+  static_assert(kS2TW == kSegCols, "a workgroup's columns are one score segment");
   using G = S2Geom<BPT, SPS>;
   constexpr int P = G::P, H = G::H;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -212,24 +274,27 @@ __global__ __launch_bounds__(kS2Threads) void k_score2(ScoreArgs a) {
   // costs one memory round trip (rows outside the waterfall / columns past F are zero and never
   // read by a valid candidate)
   if ((a.F & 3) == 0) {
-    constexpr int kVec = 3 * H * (P / 4);
-    constexpr int kIter = (kVec + kS2Threads - 1) / kS2Threads;
+    // thread -> (float4 column q4, staged row r0 + RPI it): the index math is done once, each
+    // further row is a compile-time step
+    constexpr int Q = P / 4, RPI = kS2Threads / Q, NR = 3 * H;
+    constexpr int kIter = (NR + RPI - 1) / RPI;
+    const int q4 = (int)threadIdx.x % Q, r0 = (int)threadIdx.x / Q;
+    const int col = c0 + 4 * q4;
+    const bool cok = r0 < RPI && col < a.F;
+    const float* wc = wf + col;
     float4 v[kIter];
 #pragma unroll
     for (int it = 0; it < kIter; ++it) {
-      const int i = threadIdx.x + it * kS2Threads;
+      const int rw = r0 + it * RPI;   // staged row: band m = rw / H (two compares), row in band
+      const int m = (rw >= H ? 1 : 0) + (rw >= 2 * H ? 1 : 0);
+      const int row = a0 - SPS + rw + m * (36 * SPS - H);
       v[it] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (i < kVec) {
-        const int rw = i / (P / 4), q4 = i - rw * (P / 4);
-        const int m = rw / H, rr = rw - m * H;
-        const int row = a0 + 36 * m * SPS - SPS + rr, col = c0 + 4 * q4;
-        if (row >= 0 && row < a.T && col < a.F) v[it] = *reinterpret_cast<const float4*>(wf + (int64_t)row * a.F + col);
-      }
+      if (cok && rw < NR && row >= 0 && row < a.T) v[it] = *reinterpret_cast<const float4*>(wc + row * a.F);
     }
 #pragma unroll
     for (int it = 0; it < kIter; ++it) {
-      const int i = threadIdx.x + it * kS2Threads;
-      if (i < kVec) reinterpret_cast<float4*>(tile)[i] = v[it];
+      const int rw = r0 + it * RPI;
+      if (r0 < RPI && rw < NR) reinterpret_cast<float4*>(tile)[rw * Q + q4] = v[it];
     }
   } else {
     for (int i = threadIdx.x; i < G::kFloats; i += kS2Threads) {
@@ -248,7 +313,7 @@ __global__ __launch_bounds__(kS2Threads) void k_score2(ScoreArgs a) {
   const int af = c0 + 2 * lane;
   const int nb = a.num_blocks;
   const int rows = min(kS2R, a.t0 + a.NT - a0);
-  float* out = reinterpret_cast<float*>(a.scores) + (int64_t)slot * a.NT * a.NF;
+  float* out = reinterpret_cast<float*>(a.scores) + (COMPACT ? 0 : (int64_t)slot * a.NT * a.NF);
   RowSummary* rs = a.rowsum + (int64_t)slot * a.NT;
   for (int j = w; j < rows; j += kS2Waves) {
     const int at = a0 + j;                 // wave-uniform
@@ -262,6 +327,18 @@ __global__ __launch_bounds__(kS2Threads) void k_score2(ScoreArgs a) {
       if (lo >= 0 && lo <= nb - 7) {
         // every symbol of the band and all its neighbours in range: straight-line code, so the
         // 35 loads issue together (25 differences, in the reference order)
+#if S2_LOADFIRST
+        // the band's distinct reads (30: two time neighbours are another symbol's frequency
+        // neighbour) all issue before the first difference
+        constexpr BandPlan bp = band_plan();
+        const float* bb = tb + m * H * P;
+        f32x2 v[bp.nload];
+#pragma unroll
+        for (int i = 0; i < bp.nload; ++i) v[i] = ld2<BPT>(bb + bp.row[i] * SPS * P + bp.col[i] * BPT);
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int t = 0; t < 25; ++t) score += v[bp.ctr[t]] - v[bp.nbr[t]];
+#else
 #pragma unroll
         for (int k = 0; k < 7; ++k) {
           const int tone = kCostasC[k];
@@ -272,6 +349,7 @@ __global__ __launch_bounds__(kS2Threads) void k_score2(ScoreArgs a) {
           if (k > 0) score += pw - ld2<BPT>(rp - SPS * P);
           if (k < 6) score += pw - ld2<BPT>(rp + SPS * P);
         }
+#endif
         n += 25;
       } else if (lo + 6 >= 0 && lo < nb) {
         // a band crossing the waterfall's first or last block: the reference's per-term tests
@@ -296,18 +374,30 @@ __global__ __launch_bounds__(kS2Threads) void k_score2(ScoreArgs a) {
       res[c] = (n == 0 || isnan(sc) || isinf(sc)) ? -INFINITY : sc / (float)n;
     }
     const int ti = at - a.t0;
-    float* orow = out + (int64_t)ti * a.NF;
     const bool v0 = af < a.NF, v1 = af + 1 < a.NF;
-    if (v0) orow[af] = res[0];
-    if (v1) orow[af + 1] = res[1];
     const bool p0 = v0 && passes(res[0], a.min_score, a.cmp_f64);
     const bool p1 = v1 && passes(res[1], a.min_score, a.cmp_f64);
-    const unsigned cnt = (unsigned)(__popcll(__ballot(p0)) + __popcll(__ballot(p1)));
+    const uint64_t b0 = __ballot(p0), b1 = __ballot(p1);
+    const int64_t seg = ((int64_t)slot * a.NT + ti) * a.nseg + ct;
+    if (COMPACT) {
+      // the passing scores of the segment, in column order, packed at its start: column 2l has
+      // rank popc(b0 below l) + popc(b1 below l), column 2l + 1 one more if column 2l passes
+      const uint64_t below = (1ull << lane) - 1ull;
+      const int r0 = __popcll(b0 & below) + __popcll(b1 & below);
+      float* sv = out + seg * kSegCols;
+      if (p0) sv[r0] = res[0];
+      if (p1) sv[r0 + (p0 ? 1 : 0)] = res[1];
+    } else {
+      float* orow = out + (int64_t)ti * a.NF;
+      if (v0) orow[af] = res[0];
+      if (v1) orow[af + 1] = res[1];
+    }
+    if (lane == 0) *reinterpret_cast<ulonglong2*>(a.smask + 2 * seg) = make_ulonglong2(b0, b1);
+    const unsigned cnt = (unsigned)(__popcll(b0) + __popcll(b1));
     if (cnt) {
       float mx = p0 ? res[0] : -INFINITY;
       if (p1) mx = fmaxf(mx, res[1]);
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+      mx = wave_max(mx);
       if (lane == 0) {
         atomicAdd(&rs[ti].count, cnt);
         atomicMax(&rs[ti].maxkey, order_key((double)mx));
@@ -316,7 +406,7 @@ __global__ __launch_bounds__(kS2Threads) void k_score2(ScoreArgs a) {
   }
 }
 
-template <int BPT, int SPS>
+template <int BPT, int SPS, bool COMPACT>
 hipError_t launch_score2(const SyncLaunch& L, const ScoreArgs& a0, hipStream_t s) {
   using G = S2Geom<BPT, SPS>;
   ScoreArgs a = a0;
@@ -325,15 +415,23 @@ hipError_t launch_score2(const SyncLaunch& L, const ScoreArgs& a0, hipStream_t s
   const size_t lds = sizeof(float) * G::kFloats;
   static bool attr = false;
   if (!attr) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_score2<BPT, SPS>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_score2<BPT, SPS, COMPACT>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     attr = true;
   }
   const int groups = (L.n_slots + 7) / 8;
   const int64_t blocks = (int64_t)groups * 8 * a.n_bands * a.n_ctiles;
-  hipLaunchKernelGGL((k_score2<BPT, SPS>), dim3((unsigned)blocks), dim3(kS2Threads), lds, s, a);
+  hipLaunchKernelGGL((k_score2<BPT, SPS, COMPACT>), dim3((unsigned)blocks), dim3(kS2Threads), lds, s, a);
   return hipGetLastError();
+}
+
+bool score2_path(const SyncLaunch& L) {
+  return !L.wf_f64 && L.bpt == L.sps && L.bpt >= 1 && L.bpt <= 4;
+}
+template <int B>
+hipError_t launch_score2_any(const SyncLaunch& L, const ScoreArgs& a, hipStream_t s) {
+  return score_compact(L) ? launch_score2<B, B, true>(L, a, s) : launch_score2<B, B, false>(L, a, s);
 }
 
 template <typename T, int TW>
@@ -349,6 +447,8 @@ hipError_t launch_score_t(const SyncLaunch& L, hipStream_t s) {
   a.NT = L.NT;
   a.NF = L.NF;
   a.scores = L.scores;
+  a.smask = L.smask;
+  a.nseg = n_segments(L.NF);
   a.rowsum = L.rowsum;
   a.min_score = L.min_score;
   a.cmp_f64 = L.min_score_f64;
@@ -356,16 +456,19 @@ hipError_t launch_score_t(const SyncLaunch& L, hipStream_t s) {
   hipError_t e = hipMemsetAsync(L.rowsum, 0, sizeof(RowSummary) * (size_t)L.n_slots * L.NT, s);
   if (e != hipSuccess) return e;
   if constexpr (sizeof(T) == 4) {
-    if (L.bpt == L.sps) {
+    if (score2_path(L)) {
       switch (L.bpt) {
-        case 1: return launch_score2<1, 1>(L, a, s);
-        case 2: return launch_score2<2, 2>(L, a, s);
-        case 3: return launch_score2<3, 3>(L, a, s);
-        case 4: return launch_score2<4, 4>(L, a, s);
+        case 1: return launch_score2_any<1>(L, a, s);
+        case 2: return launch_score2_any<2>(L, a, s);
+        case 3: return launch_score2_any<3>(L, a, s);
+        case 4: return launch_score2_any<4>(L, a, s);
         default: break;
       }
     }
   }
+  // k_score sets the mask bits of its passing candidates one by one
+  e = hipMemsetAsync(L.smask, 0, sizeof(uint64_t) * 2 * (size_t)L.n_slots * L.NT * a.nseg, s);
+  if (e != hipSuccess) return e;
   // rows touched by the grid: [t0 - sps, t0 + NT - 1 + 79 sps], clipped to the waterfall
   a.rlo = max(0, L.t0 - L.sps);
   const int rhi = min(L.T - 1, L.t0 + L.NT - 1 + 79 * L.sps);
@@ -399,6 +502,9 @@ struct SelectArgs {
   const RowSummary* rowsum;
   int NT;
   int32_t* tie;  // nullable: defer the order of equal scores (tie_stride(N) ints per slot)
+  const uint64_t* smask;  // [slot][NT][nseg][2] passing columns per segment
+  int nseg;
+  int compact;   // scores hold the compact segment layout (else the full grid)
 };
 
 // block-wide exclusive scans over 1024 threads (int sum and double max), via wave shuffles
@@ -423,30 +529,6 @@ __device__ int block_excl_sum(int v, int* sh, int* total) {
   __syncthreads();
   return r;
 }
-__device__ double block_excl_max(double v, double* sh, double* total) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  double x = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    double y = __shfl_up(x, o);
-    if (lane >= o) x = fmax(x, y);
-  }
-  double ex = __shfl_up(x, 1);
-  if (lane == 0) ex = -INFINITY;
-  if (lane == 63) sh[w] = x;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double acc = -INFINITY;
-    for (int i = 0; i < kSelWaves; ++i) { double t = sh[i]; sh[i] = acc; acc = fmax(acc, t); }
-    sh[kSelWaves] = acc;
-  }
-  __syncthreads();
-  const double r = fmax(sh[w], ex);
-  *total = sh[kSelWaves];
-  __syncthreads();
-  return r;
-}
-
 // bitonic sort of n items by (key asc, sec asc) in LDS (padded to a power of two <= cap)
 __device__ void bitonic(double* key, int* sec, int* pay, int n) {
   int m = 1;
@@ -472,9 +554,6 @@ __device__ void bitonic(double* key, int* sec, int* pay, int n) {
   }
 }
 
-constexpr int kSelV = 4;                        // elements per thread per chunk
-constexpr int kSelChunk = kSelThreads * kSelV;  // 4096 scores per chunk
-
 // block-wide maximum of a u64 key
 __device__ unsigned long long block_max_u64(unsigned long long v, unsigned long long* sh) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -491,21 +570,62 @@ __device__ unsigned long long block_max_u64(unsigned long long v, unsigned long 
   return m;
 }
 
+// 32 bits spread to the even bit positions of a 64-bit word
+__device__ __forceinline__ uint64_t spread32(uint32_t v) {
+  uint64_t x = v;
+  x = (x | (x << 16)) & 0x0000FFFF0000FFFFull;
+  x = (x | (x << 8)) & 0x00FF00FF00FF00FFull;
+  x = (x | (x << 4)) & 0x0F0F0F0F0F0F0F0Full;
+  x = (x | (x << 2)) & 0x3333333333333333ull;
+  x = (x | (x << 1)) & 0x5555555555555555ull;
+  return x;
+}
+// position of the k-th (0-based) set bit of w (k < popcount(w))
+__device__ __forceinline__ int select_bit(uint64_t w, int k) {
+  int pos = 0;
+#pragma unroll
+  for (int width = 32; width > 0; width >>= 1) {
+    const int c = __popcll(w & ((1ull << width) - 1ull));
+    if (k >= c) {
+      k -= c;
+      w >>= width;
+      pos += width;
+    }
+  }
+  return pos;
+}
+// rank of column col among the passing columns of a segment (masks: even / odd columns)
+__device__ __forceinline__ int seg_rank(uint64_t e, uint64_t o, int col) {
+  const int l = col >> 1;
+  const uint64_t below = (1ull << l) - 1ull;
+  return __popcll(e & ((col & 1) ? (below << 1 | 1ull) : below)) + __popcll(o & below);
+}
+
 template <typename T>
 __global__ __launch_bounds__(kSelThreads) void k_select(SelectArgs a) {
   __shared__ double s_key[kMaxCandidates + 2];
   __shared__ int s_sec[kMaxCandidates + 2];
   __shared__ int s_pay[kMaxCandidates + 2];
-  __shared__ int s_rank[kMaxCandidates];  // scan index of passing candidate #rank (rank < N)
+  __shared__ int s_rank[kMaxCandidates];     // scan index of passing candidate #rank (rank < N)
+  __shared__ T s_val[kMaxCandidates];        // its score
+  __shared__ int s_segoff[kSelThreads];      // a chunk of segments: rank of each one's first entry
+  __shared__ uint64_t s_cm[kSelThreads][2];  // its passing columns in column order (0..63, 64..127)
   __shared__ int s_isum[kSelWaves + 1];
-  __shared__ double s_dmax[kSelWaves + 1];
   __shared__ unsigned long long s_umax[kSelWaves];
   __shared__ int s_flag[6];
   __shared__ double s_am_v[kSelWaves];
   __shared__ int s_am_i[kSelWaves];
 
   const int slot = blockIdx.x;
-  const T* sc = reinterpret_cast<const T*>(a.scores) + (int64_t)slot * a.total;
+  const int nseg = a.nseg;
+  const int64_t seg0 = (int64_t)slot * a.NT * nseg;
+  const uint64_t* mk = a.smask + 2 * seg0;
+  // a passing score: segment sg (of this slot), its j-th passing column, grid column c
+  auto value = [&](int sg, int j, int c) -> T {
+    if (a.compact) return reinterpret_cast<const T*>(a.scores)[(seg0 + sg) * kSegCols + j];
+    const int row = sg / nseg;
+    return reinterpret_cast<const T*>(a.scores)[(int64_t)slot * a.total + (int64_t)row * a.NF + c];
+  };
   const RowSummary* rsum = a.rowsum + (int64_t)slot * a.NT;
   const int N = a.N;
 
@@ -531,103 +651,85 @@ __global__ __launch_bounds__(kSelThreads) void k_select(SelectArgs a) {
   __syncthreads();
   const int r_end = s_flag[4];   // rows [0, r_end) hold every rank < N
   const int g_row = s_flag[5];   // first row holding the global maximum (NT if nothing passes)
-  const double g_val = key_value(gkey);
+  const T g_val = (T)key_value(gkey);
   const int nsel = min(total_pass, N);
 
-  // ---- ordered scan of [lo, hi): ranks < N (exclusive count scan), records (strict new maxima
-  // after rank N, exclusive max scan), first-occurrence argmax (per thread, strict >)
-  int carry_cnt = 0, carry_rec = 0;
-  double carry_max = -INFINITY;
-  double best_v = -INFINITY;
-  int best_i = 0x7fffffff;
-  auto scan = [&](int64_t lo, int64_t hi) {
-    for (int64_t c0 = lo; c0 < hi; c0 += kSelChunk) {
-      T v[kSelV];
-      bool p[kSelV];
-      int lc = 0;
-      double lm = -INFINITY;
-      const int64_t i0 = c0 + (int64_t)threadIdx.x * kSelV;
-#pragma unroll
-      for (int j = 0; j < kSelV; ++j) {
-        const int64_t i = i0 + j;
-        v[j] = i < hi ? sc[i] : (T)-INFINITY;
-        p[j] = passes(v[j], a.min_score, a.cmp_f64);
-        if (p[j]) {
-          lc++;
-          lm = fmax(lm, (double)v[j]);
-          if ((double)v[j] > best_v) { best_v = (double)v[j]; best_i = (int)i; }
-        }
-      }
-      int chunk_cnt;
-      double chunk_max;
-      const int ex_cnt = block_excl_sum(lc, s_isum, &chunk_cnt);
-      const double ex_max = block_excl_max(lm, s_dmax, &chunk_max);
-      int rank = carry_cnt + ex_cnt;
-      double rm = fmax(carry_max, ex_max);
-      int nrec = 0;
-#pragma unroll
-      for (int j = 0; j < kSelV; ++j) {
-        if (!p[j]) continue;
-        if (rank < N) {
-          s_rank[rank] = (int)(i0 + j);
-        } else if ((double)v[j] > rm) {
-          nrec++;
-        }
-        rm = fmax(rm, (double)v[j]);
-        rank++;
-      }
-      if (__syncthreads_or(nrec > 0)) carry_rec++;  // only "any record" matters
-      carry_cnt += chunk_cnt;
-      carry_max = fmax(carry_max, chunk_max);
+  // ---- ranks < N in scan order, from the segment masks of rows [0, r_end): chunks of segments,
+  // an exclusive count scan gives each segment's first rank, then one thread per rank finds its
+  // segment (binary search) and column (select in the column-order mask) and loads its score
+  const int seg_end = r_end * nseg;
+  int carry = 0;
+  for (int g0 = 0; g0 < seg_end && carry < nsel; g0 += kSelThreads) {
+    const int sg = g0 + (int)threadIdx.x;
+    uint64_t e = 0, o = 0;
+    if (sg < seg_end) {
+      e = mk[2 * sg];
+      o = mk[2 * sg + 1];
     }
-  };
-  auto block_argmax = [&]() {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    double bv = best_v;
-    int bi = best_i;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const double ov = __shfl_xor(bv, o);
-      const int oi = __shfl_xor(bi, o);
-      if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
-    }
-    if (lane == 0) { s_am_v[w] = bv; s_am_i[w] = bi; }
+    int ctot;
+    const int off = carry + block_excl_sum(__popcll(e) + __popcll(o), s_isum, &ctot);
+    s_segoff[threadIdx.x] = off;
+    s_cm[threadIdx.x][0] = spread32((uint32_t)e) | (spread32((uint32_t)o) << 1);
+    s_cm[threadIdx.x][1] = spread32((uint32_t)(e >> 32)) | (spread32((uint32_t)(o >> 32)) << 1);
     __syncthreads();
-    if (threadIdx.x == 0) {
-      for (int i = 1; i < kSelWaves; ++i)
-        if (s_am_v[i] > s_am_v[0] || (s_am_v[i] == s_am_v[0] && s_am_i[i] < s_am_i[0])) {
-          s_am_v[0] = s_am_v[i];
-          s_am_i[0] = s_am_i[i];
-        }
+    const int n_here = min(kSelThreads, seg_end - g0);
+    for (int r = carry + (int)threadIdx.x; r < min(carry + ctot, nsel); r += kSelThreads) {
+      int lo = 0, hi = n_here - 1;  // the last segment whose first rank is <= r
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (s_segoff[mid] <= r) lo = mid;
+        else hi = mid - 1;
+      }
+      const int j = r - s_segoff[lo];
+      const uint64_t w0 = s_cm[lo][0];
+      const int n0 = __popcll(w0);
+      const int col = j < n0 ? select_bit(w0, j) : 64 + select_bit(s_cm[lo][1], j - n0);
+      const int sgl = g0 + lo;
+      const int row = sgl / nseg;
+      const int c = (sgl - row * nseg) * kSegCols + col;
+      s_rank[r] = row * a.NF + c;
+      s_val[r] = value(sgl, j, c);
     }
+    carry += ctot;
     __syncthreads();
-  };
+  }
 
-  scan(0, (int64_t)r_end * a.NF);
-  block_argmax();
-  // a record exists iff the first occurrence of the global maximum has rank >= N; beyond the
-  // scanned rows that is the first passing element of g_row equal to the maximum
-  const bool far = nsel > 0 && g_row >= r_end;
-  if (far) {
-    if (threadIdx.x == 0) s_am_i[0] = 0x7fffffff;
+  // ---- a record exists iff the first occurrence of the global maximum has rank >= N, i.e. iff
+  // the maximum exceeds every score of the first N (ft8_decode.py:134-137); it then ends in the heap
+  double m1 = -INFINITY;
+  for (int i = threadIdx.x; i < nsel; i += kSelThreads) m1 = fmax(m1, (double)s_val[i]);
+  {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m1 = fmax(m1, __shfl_xor(m1, o));
+    if (lane == 0) s_am_v[w] = m1;
     __syncthreads();
-    const int64_t base = (int64_t)g_row * a.NF;
+    m1 = -INFINITY;
+    for (int i = 0; i < kSelWaves; ++i) m1 = fmax(m1, s_am_v[i]);
+    __syncthreads();
+  }
+  const bool has_rec = nsel > 0 && total_pass > N && (double)g_val > m1;
+  if (threadIdx.x == 0) { s_flag[0] = 0; s_flag[1] = 0; s_flag[3] = 0; s_am_i[0] = 0x7fffffff; }
+  __syncthreads();
+  if (has_rec) {
+    // first column of row g_row holding the maximum (every earlier row's maximum is smaller)
+    const int64_t rs0 = (int64_t)g_row * nseg;
     for (int c = threadIdx.x; c < a.NF; c += kSelThreads) {
-      const T v = sc[base + c];
-      if (passes(v, a.min_score, a.cmp_f64) && (double)v == g_val) atomicMin(&s_am_i[0], (int)(base + c));
+      const int sg = (int)(rs0 + c / kSegCols), col = c % kSegCols;
+      const uint64_t e = mk[2 * sg], o = mk[2 * sg + 1];
+      if (!(((col & 1) ? o : e) >> (col >> 1) & 1ull)) continue;
+      if ((double)value(sg, seg_rank(e, o, col), c) == (double)g_val) atomicMin(&s_am_i[0], g_row * a.NF + c);
     }
     __syncthreads();
   }
-  const bool has_rec = far || carry_rec > 0;
-  if (threadIdx.x == 0) { s_flag[0] = 0; s_flag[1] = 0; s_flag[3] = 0; }
-  __syncthreads();
+  const int gi = s_am_i[0];
 
   // the heap keeps the first N; each record evicts the current maximum (the top of the first N,
   // then the previous record): the final set is the first N with its top replaced by the last
   // record (ft8_decode.py:134-137)
   for (int i = threadIdx.x; i < nsel; i += kSelThreads) {
     const int idx = s_rank[i];
-    s_key[i] = -(double)sc[idx];
+    s_key[i] = -(double)s_val[i];
     s_sec[i] = idx;
     s_pay[i] = idx;
   }
@@ -671,8 +773,7 @@ __global__ __launch_bounds__(kSelThreads) void k_select(SelectArgs a) {
       if (i != top && s_key[i] == tk) s_flag[0] = 1;
     __syncthreads();
     if (threadIdx.x == 0) {
-      const int gi = s_am_i[0];
-      s_key[top] = -(double)sc[gi];
+      s_key[top] = -(double)g_val;
       s_sec[top] = gi;
       s_pay[top] = gi;
     }
@@ -690,21 +791,28 @@ __global__ __launch_bounds__(kSelThreads) void k_select(SelectArgs a) {
     // Exact score ties in the final set: their order is the reference heap's array order, so
     // rebuild that array (heap_replay.h): the heap of the first N pushes with its root replaced by
     // the last record.
-    if constexpr (std::is_same<T, float>::value) deferred = a.tie != nullptr && nsel <= kReplayMax;
-    if (deferred) {
-      // leave the (score, scan index) order and hand the replay to one wave elsewhere: in
-      // decode_batch the first workgroups of k_llr run it beside the LLRs (the set of candidates
-      // is final; only the order of equal scores changes, which k_compact applies), in
-      // ft8_sync_select k_tie_apply runs it and reorders the list
-      int32_t* t = a.tie + (int64_t)slot * tie_stride(a.N);
-      for (int i = threadIdx.x; i < nsel; i += kSelThreads) {
-        t[i] = s_rank[i];
-        t[a.N + i] = s_pay[i];
+    if constexpr (std::is_same<T, float>::value) {
+      deferred = a.tie != nullptr && nsel <= kReplayMax;
+      if (deferred) {
+        // leave the (score, scan index) order and hand the replay to one wave elsewhere: in
+        // decode_batch the first workgroups of k_llr run it beside the LLRs (the set of candidates
+        // is final; only the order of equal scores changes, which k_compact applies), in
+        // ft8_sync_select k_tie_apply runs it and reorders the list
+        int32_t* t = a.tie + (int64_t)slot * tie_stride(a.N);
+        for (int i = threadIdx.x; i < nsel; i += kSelThreads) {
+          t[i] = s_rank[i];
+          t[a.N + i] = s_pay[i];
+          t[7 * a.N + 2 + i] = __float_as_int(s_val[i]);
+        }
+        if (threadIdx.x == 0) {
+          t[7 * a.N] = has_rec ? gi : -1;
+          t[7 * a.N + 1] = __float_as_int(g_val);
+        }
       }
-      if (threadIdx.x == 0) t[7 * a.N] = has_rec ? s_am_i[0] : -1;
-    } else {
+    }
+    if (!deferred) {
       for (int i = threadIdx.x; i < nsel; i += kSelThreads) {
-        s_key[i] = -(double)sc[s_rank[i]];
+        s_key[i] = -(double)s_val[i];
         s_sec[i] = s_rank[i];
       }
       __syncthreads();
@@ -752,8 +860,7 @@ __global__ __launch_bounds__(kSelThreads) void k_select(SelectArgs a) {
               }
               c = 2 * c + 1;
             }
-            const int gi = s_am_i[0];
-            s_key[0] = -(double)sc[gi];
+            s_key[0] = -(double)g_val;
             s_sec[0] = gi;
           }
         }
@@ -938,6 +1045,10 @@ __global__ __launch_bounds__(kSelThreads) void k_topk(SelectArgs a) {
 
 }  // namespace
 
+// the compact layout needs k_score2 (whole-segment writes) and the reference selection (k_topk
+// reads the full grid)
+bool score_compact(const SyncLaunch& L) { return L.compact && !L.topk && score2_path(L); }
+
 hipError_t launch_score(const SyncLaunch& L, hipStream_t s) {
   if (L.NT <= 0 || L.NF <= 0 || L.n_slots <= 0) return hipSuccess;
   if (L.wf_f64) return launch_score_t<double, 32>(L, s);
@@ -974,6 +1085,9 @@ hipError_t launch_select(const SyncLaunch& L, hipStream_t s) {
   a.rowsum = L.rowsum;
   a.tie = L.tie;
   a.NT = max(L.NT, 0);
+  a.smask = L.smask;
+  a.nseg = n_segments(a.NF);
+  a.compact = score_compact(L) ? 1 : 0;
   if (L.topk) {
     if (L.wf_f64)
       hipLaunchKernelGGL(k_topk<double>, dim3(L.n_slots), dim3(kSelThreads), 0, s, a);

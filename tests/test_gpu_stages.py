@@ -277,3 +277,30 @@ def test_max_candidates_limit_is_an_error(gpu):
     assert decode_ft8_message(x, 12000, max_candidates=lim, min_score=100) == []
     with pytest.raises(ValueError, match="max_candidates"):
         decode_ft8_message(x, 12000, max_candidates=lim + 1, min_score=100)
+
+
+def test_compact_scores_select_like_the_full_grid(gpu, oracle):
+    """Without a caller grid the score kernel writes only the passing scores of each 128-column
+    segment plus its column mask, and k_select walks the masks; with a grid it reads the full grid.
+    Both give the oracle's selection (ft8_decode.py:102-149) on dense, sparse and record-making
+    waterfalls, ragged segment tails (NF not a multiple of 128) and N from 1 to the 4096 limit."""
+    from ft8_demodulator_amd import _device
+    rng = np.random.default_rng(77)
+    n = 0
+    for trial, (F, T) in enumerate(((135, 186), (520, 186), (1920, 186), (1000, 150), (300, 400))):
+        mag = (rng.standard_normal((F, T)) * 6.0 - 60.0).astype(np.float32)
+        if trial % 2 == 0:
+            mag[:, -40:] += np.linspace(0, 20, 40, dtype=np.float32)[None, :]  # late records
+        wf = _wf(mag, 2, 2)
+        grid = oracle.score_grid(mag, 2, 2)
+        NF = grid.shape[1]
+        for N, ms in ((1, 0), (7, 2), (300, 2), (300, 6), (4096, -100), (2000, 1)):
+            idx, sc, _ = oracle.select(grid, N, ms)
+            exp = [(int(i // NF) - 20, int(i % NF)) for i in idx]
+            compact, _, w1 = _device.sync_select(wf, N, ms)
+            full, _, w2 = _device.sync_select(wf, N, ms, want_grid=True)
+            assert compact == full and w1 == w2, (trial, N, ms)
+            assert [(c[0], c[1]) for c in compact] == exp, (trial, N, ms)
+            assert np.array_equal(np.array([c[2] for c in compact], dtype=np.float32).reshape(-1), sc), (trial, N, ms)
+            n += 1
+    assert n == 30
