@@ -143,7 +143,7 @@ def lib():
 
 
 # csrc files hashed into FT8_BUILD_ID, in the Makefile's ID_FILES order
-_ID_FILES = ("capi.hip", "stft.hip", "sync.hip", "bp.hip", "tx.hip", "subtract.hip", "drift.hip",
+_ID_FILES = ("capi.hip", "stft.hip", "stft3840.hip", "sync.hip", "bp.hip", "tx.hip", "subtract.hip", "drift.hip",
              "ft8_internal.h", "ft8_ldpc_tables.h", "tx_device.h", "heap_replay.h", "../../include/ft8hip.h",
              "Makefile")
 

@@ -50,6 +50,10 @@ constexpr int kProdGroup = BP_PROD_GROUP;
 #ifndef BP_WAVES_PER_EU
 #define BP_WAVES_PER_EU 4
 #endif
+#ifndef BP_FOLD_HALF
+#define BP_FOLD_HALF 1  // fast_tanh's -1/2 argument scaling folded into its polynomial constants
+#endif
+[[maybe_unused]] constexpr double kClip2 = 2.0 * 4.97;  // exact: twice fast_tanh's clip bound
 #ifndef BP_GRID_CUS
 #define BP_GRID_CUS 256  // CUs the persistent grid covers (experiments only)
 #endif
@@ -98,6 +102,28 @@ __device__ __forceinline__ double pymax4(double a, double b, double c, double d)
 // caller scales by -2, ldpc_decoder.py:108).  On the fast path every quotient is normal, so
 // RN(x / (-b/2)) == -2 RN(x/b) exactly and the scaling costs nothing; the full path divides by
 // b = -2 y (exact) and scales the quotient.
+// the short sequence alone, for callers that established its preconditions themselves
+template <int N>
+__device__ __forceinline__ void div_fast(double* q, const double* x, const double* y) {
+  double r[N], e[N], m[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) r[i] = __builtin_amdgcn_rcp(y[i]);
+#pragma unroll
+  for (int i = 0; i < N; ++i) e[i] = __builtin_fma(-y[i], r[i], 1.0);
+#pragma unroll
+  for (int i = 0; i < N; ++i) r[i] = __builtin_fma(r[i], e[i], r[i]);
+#pragma unroll
+  for (int i = 0; i < N; ++i) e[i] = __builtin_fma(-y[i], r[i], 1.0);
+#pragma unroll
+  for (int i = 0; i < N; ++i) r[i] = __builtin_fma(r[i], e[i], r[i]);
+#pragma unroll
+  for (int i = 0; i < N; ++i) m[i] = x[i] * r[i];
+#pragma unroll
+  for (int i = 0; i < N; ++i) e[i] = __builtin_fma(-y[i], m[i], x[i]);
+#pragma unroll
+  for (int i = 0; i < N; ++i) q[i] = __builtin_fma(e[i], r[i], m[i]);
+}
+
 template <int N, bool NEG2 = false>
 __device__ __forceinline__ void div_rn(double* q, const double* x, const double* y_in) {
   // |x| < 2^900 always holds here (clamped / bounded inputs).  A NaN numerator yields NaN on either
@@ -619,9 +645,16 @@ __global__ __launch_bounds__(kWave, BP_WAVES_PER_EU) void k_bp(BpArgs a) {
         const double T0 = (c + t1) + t2, T1 = c0 + t2, T2 = c0 + t1;
         // fast_tanh's np.clip (no NaN reaches here)
         if (j < kVarSlots - 1 || var2) {
+#if BP_FOLD_HALF
+          // y = clip(T, -2 c, 2 c) = -2 clip(-T / 2, -c, c), c = 4.97: the -1/2 goes into phase C
+          *(__attribute__((address_space(3))) double*)(uintptr_t)a0 = __builtin_fmin(__builtin_fmax(T0, -kClip2), kClip2);
+          *(__attribute__((address_space(3))) double*)(uintptr_t)a1 = __builtin_fmin(__builtin_fmax(T1, -kClip2), kClip2);
+          *(__attribute__((address_space(3))) double*)(uintptr_t)a2 = __builtin_fmin(__builtin_fmax(T2, -kClip2), kClip2);
+#else
           *(__attribute__((address_space(3))) double*)(uintptr_t)a0 = __builtin_fmin(__builtin_fmax(-T0 / 2, -4.97), 4.97);
           *(__attribute__((address_space(3))) double*)(uintptr_t)a1 = __builtin_fmin(__builtin_fmax(-T1 / 2, -4.97), 4.97);
           *(__attribute__((address_space(3))) double*)(uintptr_t)a2 = __builtin_fmin(__builtin_fmax(-T2 / 2, -4.97), 4.97);
+#endif
         }
       }
       hd[kVarSlots - 1] &= var2_mask;
@@ -648,6 +681,39 @@ __global__ __launch_bounds__(kWave, BP_WAVES_PER_EU) void k_bp(BpArgs a) {
 #pragma unroll
       for (int i = 0; i < kEdgeSlots; ++i) x[i] = *(lds_f64*)(uintptr_t)(la + 512u * i);
       // variable -> check messages: toc = fast_tanh(-Tnm / 2), three interleaved divisions at a time
+#if BP_FOLD_HALF
+      // From y = -2 x (x the reference's clipped argument): with z = RN(y y) = 4 RN(x x), every step
+      // of fast_tanh's polynomials (ldpc_decoder.py:11-20) is the reference's step scaled by a power
+      // of two, so na = -A / 32 and nb = B / -32 exactly for
+      //   A = y (15120 + z (420 + z)),   B = -30240 + z (-3360 + z (-30)),
+      // and toc = RN(na / nb) = RN(A / B): the same real quotient.  The scalings are exact while
+      // nothing underflows, which |A| >= 2^-480 (so |y| >= 2^-496) guarantees for the whole wave;
+      // the same bound admits the short division.  Otherwise (tiny or zero arguments) the group
+      // runs the reference form on x = -y / 2.
+#pragma unroll
+      for (int g = 0; g < kEdgeSlots; g += kDivGroup) {
+        double na[kDivGroup], nb[kDivGroup];
+        double mn = INFINITY;
+#pragma unroll
+        for (int i = 0; i < kDivGroup; ++i) {
+          const double yv = x[g + i], z = yv * yv;
+          na[i] = yv * (15120.0 + z * (420.0 + z));
+          nb[i] = -30240.0 + z * (-3360.0 + z * -30.0);
+          mn = __builtin_fmin(mn, __builtin_fabs(na[i]));
+        }
+        if (__ballot(mn >= 0x1p-480) == __builtin_amdgcn_read_exec()) {
+          div_fast<kDivGroup>(&x[g], na, nb);
+        } else {
+#pragma unroll
+          for (int i = 0; i < kDivGroup; ++i) {
+            const double xv = -0.5 * x[g + i], x2 = xv * xv;
+            na[i] = xv * (945.0 + x2 * (105.0 + x2));
+            nb[i] = 945.0 + x2 * (420.0 + x2 * 15.0);
+          }
+          div_rn<kDivGroup>(&x[g], na, nb);
+        }
+      }
+#else
 #pragma unroll
       for (int g = 0; g < kEdgeSlots; g += kDivGroup) {
         double na[kDivGroup], nb[kDivGroup];
@@ -659,6 +725,7 @@ __global__ __launch_bounds__(kWave, BP_WAVES_PER_EU) void k_bp(BpArgs a) {
         }
         div_rn<kDivGroup>(&x[g], na, nb);
       }
+#endif
 #pragma unroll
       for (int i = 0; i < kEdgeSlots; ++i)
         if (i < kEdgeSlots - 1 || lane + kWave * i < FT8_LDPC_E)

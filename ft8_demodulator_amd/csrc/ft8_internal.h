@@ -52,6 +52,10 @@ struct StftLaunch {
   FftPlan plan;
 };
 hipError_t launch_stft(const StftLaunch& a, hipStream_t s);
+// the production geometry (real float32 / int16 input, nfft 3840, nperseg 1920, hop 960) with packed
+// float32 complex arithmetic (stft3840.hip)
+bool stft3840_eligible(const StftLaunch& a);
+hipError_t launch_stft3840(const StftLaunch& a, hipStream_t s);
 
 // ---- sync score + selection ----------------------------------------------------------------
 // Per (slot, time row) summary written by k_score for k_select: how many grid points of the row

@@ -26,6 +26,9 @@ namespace ft8 {
 namespace {
 
 constexpr int kThreads = 256;
+#ifndef STFT_PACKED
+#define STFT_PACKED 1  // the production geometry runs stft3840.hip's packed kernel
+#endif
 
 template <typename T>
 __device__ __forceinline__ cplx<T> cadd(cplx<T> a, cplx<T> b) { return {a.x + b.x, a.y + b.y}; }
@@ -1023,6 +1026,9 @@ hipError_t launch_stft(const StftLaunch& L, hipStream_t s) {
     }
   }
   // production geometry: 12 kHz, bins_per_tone = steps_per_symbol = 2 (pairs need an even stride)
+#if STFT_PACKED
+  if (stft3840_eligible(L)) return launch_stft3840(L, s);
+#endif
   if (!L.argmax && (L.dtype == FT8_F32 || L.dtype == FT8_I16) && L.nfft == 2 * k38P && L.nperseg == k38P && L.hop == 960 &&
       a.P == k38P && (L.slot_stride % 2) == 0) {
     const int chunks = (a.nt_out + k38Chunk - 1) / k38Chunk;

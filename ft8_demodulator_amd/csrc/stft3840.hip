@@ -1,0 +1,428 @@
+// stft3840.hip -- the production STFT geometry (12 kHz, bins_per_tone = steps_per_symbol = 2: real
+// input, nfft = 3840, nperseg = 1920, hop = 960) with packed float32 complex arithmetic (gfx950).
+//
+// Same transform as stft.hip's generic path (calculate_spectrogram, reference
+// spectrogram_analyse.py:19-66, and the f >= 0 / band / time masks of ft8_decode.py:322-341): the
+// 3840-point real FFT of each Hann-windowed frame is a P = 1920-point complex FFT of
+// z[n] = w x[2n] + i w x[2n+1] plus a post-twiddle pass, P = 16 x 8 x 15 in three Stockham stages
+// with compile-time radices, then |X|^2 / (sum w)^2 -> 10 log10(1e-12 + .) written once.
+//
+// A complex value lives in one aligned register pair (re, im) and every complex operation is a
+// VOP3P packed float32 instruction: an addition or subtraction is one v_pk_add_f32; a product is
+// v_pk_mul_f32 + v_pk_fma_f32 with operand selection (op_sel) and per-half negation (neg_lo/hi)
+// doing the swap and the sign; multiplications by -i and conjugations fold into the neighbouring
+// addition.  The compiler does not form these selections itself (it builds the swapped operand
+// with extra moves), so the few instructions that need them are written as inline assembly.
+// This file is built with packed math enabled and FMA contraction (Makefile); the FFT is not
+// pocketfft in either case, and tests bound the dB error (tests/test_gpu_stft.py).
+//
+// Work decomposition (unchanged from the scalar kernel it replaces): 128 threads, one butterfly
+// per thread per stage (stage 2 runs two), ping-pong LDS buffers, twiddles formed in registers by
+// recurrence from per-thread seeds; a workgroup walks a run of consecutive frames of one slot and
+// keeps the raw samples in registers, since a frame's second half is the next frame's first half
+// (each run reads (c + 1) / c of its samples), prefetching the next frame's new samples.
+#include "ft8_internal.h"
+
+namespace ft8 {
+namespace {
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+// ---- packed complex helpers -------------------------------------------------------------------
+// (a.x b.x - a.y b.y, a.x b.y + a.y b.x)
+__device__ __forceinline__ f2 cmul(f2 a, f2 b) {
+  f2 t, r;
+  asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(t) : "v"(a), "v"(b));
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[1,0,0]" : "=v"(r) : "v"(a), "v"(b), "v"(t));
+  return r;
+}
+// a + (-i) b = (a.x + b.y, a.y - b.x)
+__device__ __forceinline__ f2 add_mi(f2 a, f2 b) {
+  f2 r;
+  asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+// a - (-i) b = (a.x - b.y, a.y + b.x)
+__device__ __forceinline__ f2 sub_mi(f2 a, f2 b) {
+  f2 r;
+  asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+// a + conj(b) = (a.x + b.x, a.y - b.y)
+__device__ __forceinline__ f2 add_cj(f2 a, f2 b) {
+  f2 r;
+  asm("v_pk_add_f32 %0, %1, %2 neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+// a - conj(b) = (a.x - b.x, a.y + b.y)
+__device__ __forceinline__ f2 sub_cj(f2 a, f2 b) {
+  f2 r;
+  asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+// (a.x + b.y, a.x - b.y) and (a.y - b.x, a.y + b.x): the real and imaginary parts of a + (-i) b
+// and a - (-i) b side by side
+__device__ __forceinline__ f2 re_pm(f2 a, f2 b) {
+  f2 r;
+  asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[0,1] neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ f2 im_mp(f2 a, f2 b) {
+  f2 r;
+  asm("v_pk_add_f32 %0, %1, %2 op_sel:[1,0] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ f2 splat(float s) { return f2{s, s}; }
+
+// ---- in-register DFTs (W_R = exp(-2 pi i / R)) --------------------------------------------------
+__device__ __forceinline__ void dft4(f2* a) {
+  const f2 t0 = a[0] + a[2], t1 = a[0] - a[2], t2 = a[1] + a[3], d = a[1] - a[3];
+  a[0] = t0 + t2;
+  a[2] = t0 - t2;
+  a[1] = add_mi(t1, d);
+  a[3] = sub_mi(t1, d);
+}
+__device__ __forceinline__ void dft8(f2* a) {
+  const f2 r = splat(0.70710678118654752440f);
+  f2 e[4] = {a[0], a[2], a[4], a[6]};
+  f2 o[4] = {a[1], a[3], a[5], a[7]};
+  dft4(e);
+  dft4(o);
+  const f2 w1 = add_mi(o[1], o[1]) * r;  // o1 W_8 = r (o1.x + o1.y, o1.y - o1.x)
+  const f2 v3 = add_mi(o[3], o[3]) * r;  // o3 W_8^3 = -i (o3 W_8)
+  a[0] = e[0] + o[0];
+  a[4] = e[0] - o[0];
+  a[1] = e[1] + w1;
+  a[5] = e[1] - w1;
+  a[2] = add_mi(e[2], o[2]);
+  a[6] = sub_mi(e[2], o[2]);
+  a[3] = add_mi(e[3], v3);
+  a[7] = sub_mi(e[3], v3);
+}
+__device__ __forceinline__ void dft3(f2* a) {
+  const f2 t = a[1] + a[2], d = (a[1] - a[2]) * splat(0.86602540378443864676f);
+  const f2 m = a[0] - splat(0.5f) * t;
+  a[0] = a[0] + t;
+  a[1] = add_mi(m, d);
+  a[2] = sub_mi(m, d);
+}
+__device__ __forceinline__ void dft5(f2* a) {
+  const f2 c1 = splat(0.30901699437494742410f), c2 = splat(-0.80901699437494742410f);
+  const f2 s1 = splat(0.95105651629515357212f), s2 = splat(0.58778525229247312917f);
+  const f2 t1 = a[1] + a[4], t2 = a[2] + a[3], t3 = a[1] - a[4], t4 = a[2] - a[3];
+  const f2 b1 = a[0] + c1 * t1 + c2 * t2;
+  const f2 b2 = a[0] + c2 * t1 + c1 * t2;
+  const f2 e1 = s1 * t3 + s2 * t4;
+  const f2 e2 = s2 * t3 - s1 * t4;
+  a[0] = a[0] + (t1 + t2);
+  a[1] = add_mi(b1, e1);
+  a[4] = sub_mi(b1, e1);
+  a[2] = add_mi(b2, e2);
+  a[3] = sub_mi(b2, e2);
+}
+// 15 = 3 x 5 prime-factor (no internal twiddles): n = (5 n1 + 3 n2) mod 15, k = (10 k1 + 6 k2) mod 15
+__device__ __forceinline__ void dft15(const f2* x, f2* y) {
+  f2 Y[3][5];
+#pragma unroll
+  for (int n1 = 0; n1 < 3; ++n1) {
+#pragma unroll
+    for (int n2 = 0; n2 < 5; ++n2) Y[n1][n2] = x[(5 * n1 + 3 * n2) % 15];
+    dft5(Y[n1]);
+  }
+#pragma unroll
+  for (int k2 = 0; k2 < 5; ++k2) {
+    f2 v[3] = {Y[0][k2], Y[1][k2], Y[2][k2]};
+    dft3(v);
+#pragma unroll
+    for (int k1 = 0; k1 < 3; ++k1) y[(10 * k1 + 6 * k2) % 15] = v[k1];
+  }
+}
+__device__ __forceinline__ f2 w16(int m) {  // exp(-2 pi i m / 16), m in [0, 9]
+  constexpr float c[10] = {1.0f, 0.92387953251128675613f, 0.70710678118654752440f, 0.38268343236508977173f,
+                           0.0f, -0.38268343236508977173f, -0.70710678118654752440f, -0.92387953251128675613f,
+                           -1.0f, -0.92387953251128675613f};
+  constexpr float sn[10] = {0.0f, -0.38268343236508977173f, -0.70710678118654752440f, -0.92387953251128675613f,
+                            -1.0f, -0.92387953251128675613f, -0.70710678118654752440f, -0.38268343236508977173f,
+                            0.0f, 0.38268343236508977173f};
+  return f2{c[m], sn[m]};
+}
+// 16-point DFT of x[0..7] with x[8..15] = 0 (4 x 4 Cooley-Tukey), y in natural order
+__device__ __forceinline__ void dft16_half(const f2* x, f2* y) {
+  f2 A[4][4];  // [n2][k1]
+#pragma unroll
+  for (int n2 = 0; n2 < 4; ++n2) {
+    const f2 a = x[n2], b = x[4 + n2];
+    A[n2][0] = a + b;
+    A[n2][1] = add_mi(a, b);
+    A[n2][2] = a - b;
+    A[n2][3] = sub_mi(a, b);
+  }
+#pragma unroll
+  for (int n2 = 1; n2 < 4; ++n2)
+#pragma unroll
+    for (int k1 = 1; k1 < 4; ++k1)
+      if (n2 * k1 != 4) A[n2][k1] = cmul(A[n2][k1], w16(n2 * k1));
+  // k1 = 2: A[2][2] carries W_16^4 = -i, folded into its butterflies
+#pragma unroll
+  for (int k1 = 0; k1 < 4; ++k1) {
+    if (k1 == 2) {
+      const f2 t0 = add_mi(A[0][2], A[2][2]), t1 = sub_mi(A[0][2], A[2][2]);
+      const f2 t2 = A[1][2] + A[3][2], d = A[1][2] - A[3][2];
+      y[2] = t0 + t2;
+      y[10] = t0 - t2;
+      y[6] = add_mi(t1, d);
+      y[14] = sub_mi(t1, d);
+    } else {
+      f2 v[4] = {A[0][k1], A[1][k1], A[2][k1], A[3][k1]};
+      dft4(v);
+#pragma unroll
+      for (int k2 = 0; k2 < 4; ++k2) y[k1 + 4 * k2] = v[k2];
+    }
+  }
+}
+
+template <typename InT>
+__device__ __forceinline__ f2 load_pair(const InT* x, int64_t n0) {
+  if constexpr (sizeof(InT) == 4) {
+    const float2 v = *reinterpret_cast<const float2*>(x + n0);
+    return f2{v.x, v.y};
+  } else {
+    const short2 v = *reinterpret_cast<const short2*>(x + n0);
+    return f2{(float)v.x / 32767.0f, (float)v.y / 32767.0f};  // read_wave_file: float32(x) / iinfo(int16).max
+  }
+}
+
+constexpr int kP = 1920;
+constexpr int kThreads38 = 128;
+constexpr int kChunk = 8;  // frames per workgroup (24 workgroups per slot at 186 frames)
+
+struct Args {
+  const void* samples;
+  int64_t slot_stride;
+  int t_lo, f_lo, nf_out, nt_out;
+  const float* window;
+  float scale;
+  float* out;
+  const f2* tw;    // W_1920^m
+  const f2* post;  // W_3840^k, k in [0, 1920]
+};
+
+__device__ __forceinline__ int pidx(int i) { return i + (i >> 4); }
+
+#ifndef S38_ONEBUF
+#define S38_ONEBUF 0  // 1: one LDS buffer (every stage loads its inputs, barrier, stores): 16 KB per workgroup
+#endif
+#ifndef S38_WINREG
+#define S38_WINREG 1  // the thread's window values stay in registers (0: reloaded from L1 each frame)
+#endif
+
+template <typename InT>
+__global__ __launch_bounds__(kThreads38) void k_stft3840p(Args a) {
+  // bufA is read and written with pidx padding: the stage-1 writes go out with a 16-complex stride
+  // across lanes (128 B: 32-way bank conflicts unpadded)
+  __shared__ f2 bufA[kP + kP / 16 + 1];
+#if S38_ONEBUF
+  f2* const bufB = bufA;
+#define S38_BIDX(i) pidx(i)
+#else
+  __shared__ f2 bufB[kP];
+#define S38_BIDX(i) (i)
+#endif
+  const int t = threadIdx.x;
+  const int chunks = (a.nt_out + kChunk - 1) / kChunk;
+  const int slot = blockIdx.x / chunks;
+  const int c = blockIdx.x - slot * chunks;
+  const int f_begin = c * kChunk, f_end = min(a.nt_out, f_begin + kChunk);
+  // twiddle seeds: stage 2 W_128^k (k = t % 16), stage 3 W_1920^t, epilogue W_3840^(f_lo + t) and
+  // its 128-bin step; their powers are formed by complex recurrence each frame (relative error
+  // ~15 ulp, far inside the dB tolerance)
+  f2 s2 = a.tw[15 * (t & 15)], s3 = a.tw[t];
+  const bool rec_post = a.f_lo + a.nf_out <= kP;
+  const bool full = a.f_lo == 0 && a.nf_out == kP;  // every f >= 0 bin kept (no band mask)
+  // 10 log10(v) = (10 log10 2) log2(v): v_log_f32 on a normal argument (v >= 1e-12)
+  constexpr float kDb = 3.0102999566398119521f;
+  f2 p0 = a.post[min(a.f_lo + t, kP)];
+  const f2 pstep = a.post[kThreads38];
+  const f2 qscale = splat(0.25f * a.scale);  // |2 X|^2 / 4 / (sum w)^2 (powers of two: exact)
+
+  // the window of the thread's 8 stage-1 pairs
+  const bool s1 = t < 120;
+  auto window = [&](int r) -> f2 {
+    const int n = t + 120 * r;
+    return *reinterpret_cast<const f2*>(a.window + 2 * n);
+  };
+#if S38_WINREG
+  f2 win[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) win[r] = s1 ? window(r) : splat(0.0f);
+#endif
+  const InT* xs = reinterpret_cast<const InT*>(a.samples) + (int64_t)slot * a.slot_stride;
+  f2 raw[8];  // raw pairs (x[2n], x[2n+1]), n = t + 120 r, of the current frame
+  {
+    const int64_t base = (int64_t)(a.t_lo + f_begin) * 960;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) raw[r] = s1 ? load_pair<InT>(xs, base + 2 * (t + 120 * r)) : splat(0.0f);
+  }
+  for (int f = f_begin; f < f_end; ++f) {
+    // re-opaque the seeds so the per-frame twiddle powers are not hoisted into ~50 live registers
+    asm volatile("" : "+v"(s2), "+v"(s3), "+v"(p0));
+    // prefetch the next frame's 4 new pairs (n + 480 = t + 120 (r + 4))
+    f2 nx[4];
+    const bool more = f + 1 < f_end;
+    if (s1 && more) {
+      const int64_t base = (int64_t)(a.t_lo + f + 1) * 960;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) nx[r] = load_pair<InT>(xs, base + 2 * (t + 120 * (r + 4)));
+    }
+    // stage 1: radix 16, Ns = 1: inputs z[t + 120 r] (r >= 8 is zero padding) -> bufA[16 t + k]
+    __syncthreads();  // the previous frame's epilogue has finished reading bufA
+    if (s1) {
+      f2 z[8], y[16];
+#pragma unroll
+#if S38_WINREG
+      for (int r = 0; r < 8; ++r) z[r] = win[r] * raw[r];
+#else
+      for (int r = 0; r < 8; ++r) z[r] = window(r) * raw[r];
+#endif
+      dft16_half(z, y);
+#pragma unroll
+      for (int k = 0; k < 16; ++k) bufA[pidx(16 * t + k)] = y[k];
+    }
+    __syncthreads();
+    // stage 2: radix 8, Ns = 16: j in {t, t + 128} (j < 240)
+#if S38_ONEBUF
+    f2 v2[2][8];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int j = t + 128 * h;
+      if (j < 240) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) v2[h][r] = bufA[pidx(j + 240 * r)];
+      }
+    }
+    __syncthreads();  // every stage-2 input is in registers before the buffer is overwritten
+#endif
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int j = t + 128 * h;
+      if (j < 240) {
+#if S38_ONEBUF
+        f2* v = v2[h];
+#else
+        f2 v[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) v[r] = bufA[pidx(j + 240 * r)];
+#endif
+        if ((j & 15) != 0) {
+          f2 w = s2;  // W_128^(r k)
+#pragma unroll
+          for (int r = 1; r < 8; ++r) {
+            v[r] = cmul(v[r], w);
+            if (r < 7) w = cmul(w, s2);
+          }
+        }
+        dft8(v);
+        const int d0 = (j >> 4) * 128 + (j & 15);
+#pragma unroll
+        for (int r = 0; r < 8; ++r) bufB[S38_BIDX(d0 + 16 * r)] = v[r];
+      }
+    }
+    __syncthreads();
+    // stage 3: radix 15, Ns = 128: j = t -> natural order into bufA
+    {
+      f2 v[15], y[15];
+#pragma unroll
+      for (int r = 0; r < 15; ++r) v[r] = bufB[S38_BIDX(t + 128 * r)];
+#if S38_ONEBUF
+      __syncthreads();
+#endif
+      if (t != 0) {
+        f2 w = s3;  // W_1920^(r t)
+#pragma unroll
+        for (int r = 1; r < 15; ++r) {
+          v[r] = cmul(v[r], w);
+          if (r < 14) w = cmul(w, s3);
+        }
+      }
+      dft15(v, y);
+#pragma unroll
+      for (int r = 0; r < 15; ++r) bufA[pidx(t + 128 * r)] = y[r];
+    }
+    __syncthreads();
+    // epilogue: real-signal spectrum X[k] = (s - i W_N^k d) / 2 with s = Z[k] + conj Z[P-k],
+    // d = Z[k] - conj Z[P-k]; power, dB, kept bins
+    float* out = a.out + ((int64_t)slot * a.nt_out + f) * a.nf_out;
+    if (full) {
+      // k and P - k share s and d: since W_N^(P-k) = -conj(W_N^k), 2 X[P-k] = conj(s + i W d)... the
+      // two spectra are (s.x + wd.y, s.y - wd.x) and (s.x - wd.y, -(s.y + wd.x)) for wd = W_N^k d;
+      // their real parts and imaginary parts are formed side by side, so both powers come from one
+      // packed multiply-add
+      f2 pw_k = p0;  // W_3840^k, k = t + 128 j
+      for (int k = t; k <= kP / 2; k += kThreads38) {
+        const f2 A = bufA[pidx(k)];
+        const f2 B = bufA[pidx(k == 0 ? 0 : kP - k)];
+        const f2 sm = add_cj(A, B), df = sub_cj(A, B);
+        const f2 wd = cmul(pw_k, df);
+        pw_k = cmul(pw_k, pstep);
+        const f2 re = re_pm(sm, wd), im = im_mp(sm, wd);   // (X1.x, X2.x), (X1.y, -X2.y)
+        const f2 p = (re * re + im * im) * qscale + splat(1e-12f);
+        const float d1 = kDb * __builtin_amdgcn_logf(p.x), d2 = kDb * __builtin_amdgcn_logf(p.y);
+        out[k] = d1;
+        if (k != 0 && k != kP / 2) out[kP - k] = d2;
+      }
+    } else {
+      f2 pw_k = p0;  // W_3840^k for k = f_lo + i (recurrence over i += 128)
+      for (int i = t; i < a.nf_out; i += kThreads38) {
+        const int k = a.f_lo + i;
+        const int kk = (k <= kP) ? k : 2 * kP - k;
+        const f2 A = bufA[pidx(kk == kP ? 0 : kk)];
+        const f2 B = bufA[pidx(kk == 0 ? 0 : kP - kk)];
+        const f2 sm = add_cj(A, B), df = sub_cj(A, B);
+        const f2 wd = cmul(rec_post ? pw_k : a.post[kk], df);
+        pw_k = cmul(pw_k, pstep);
+        const f2 X = add_mi(sm, wd);
+        const f2 q = X * X;
+        const float pw = (q.x + q.y) * qscale.x + 1e-12f;
+        out[i] = kDb * __builtin_amdgcn_logf(pw);
+      }
+    }
+    // slide the window: pairs r >= 4 become r - 4, the prefetched pairs fill r = 4..7
+    if (more) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        raw[r] = raw[r + 4];
+        raw[r + 4] = nx[r];
+      }
+    }
+  }
+}
+
+}  // namespace
+
+bool stft3840_eligible(const StftLaunch& L) {
+  return !L.argmax && !L.plan.dft && (L.dtype == FT8_F32 || L.dtype == FT8_I16) && L.nfft == 2 * kP &&
+         L.nperseg == kP && L.hop == 960 && L.plan.P == kP && (L.slot_stride % 2) == 0;
+}
+
+hipError_t launch_stft3840(const StftLaunch& L, hipStream_t s) {
+  Args a{};
+  a.samples = L.samples;
+  a.slot_stride = L.slot_stride;
+  a.t_lo = L.t_lo;
+  a.f_lo = L.f_lo;
+  a.nf_out = L.f_hi - L.f_lo;
+  a.nt_out = L.t_hi - L.t_lo;
+  a.window = reinterpret_cast<const float*>(L.window);
+  a.scale = (float)L.scale;
+  a.out = reinterpret_cast<float*>(L.out);
+  a.tw = reinterpret_cast<const f2*>(L.plan.tw);
+  a.post = reinterpret_cast<const f2*>(L.plan.post);
+  if (a.nt_out <= 0 || a.nf_out <= 0 || L.n_slots <= 0) return hipSuccess;
+  const int chunks = (a.nt_out + kChunk - 1) / kChunk;
+  const dim3 grid((unsigned)(chunks * L.n_slots));
+  if (L.dtype == FT8_F32) hipLaunchKernelGGL(k_stft3840p<float>, grid, dim3(kThreads38), 0, s, a);
+  else hipLaunchKernelGGL(k_stft3840p<int16_t>, grid, dim3(kThreads38), 0, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace ft8

@@ -8,6 +8,6 @@ mkdir -p ../../variants ../../build/var
 F=$2
 EXTRA=$(make -s -p 2>/dev/null | sed -n "s/^EXTRA_$F := //p" | head -1)
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -Wall -Wno-unused-result $EXTRA $3 -c $F.hip -o ../../build/var/$1_$F.o
-OBJS=$(for s in capi stft sync bp tx subtract drift; do if [ $s = $F ]; then echo ../../build/var/$1_$F.o; else echo ../../build/$s.o; fi; done)
+OBJS=$(for s in capi stft stft3840 sync bp tx subtract drift; do if [ $s = $F ]; then echo ../../build/var/$1_$F.o; else echo ../../build/$s.o; fi; done)
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o ../../variants/$1.so $OBJS
 echo variants/$1.so
