@@ -30,7 +30,7 @@ __constant__ uint16_t kChkStartD[FT8_LDPC_M + 1] = FT8_CHK_START_INIT;
 __constant__ uint8_t kEdgeVarD[FT8_LDPC_E] = FT8_EDGE_VAR_INIT;
 __constant__ uint16_t kVarEdgeD[FT8_LDPC_N * 3] = FT8_VAR_EDGE_INIT;
 __constant__ uint8_t kEdgeChkD[FT8_LDPC_E] = FT8_EDGE_CHK_INIT;
-__constant__ int kGrayD[8] = {0, 1, 3, 2, 5, 6, 4, 7};  // ft8_decode.py:39
+constexpr int kGrayD[8] = {0, 1, 3, 2, 5, 6, 4, 7};  // ft8_decode.py:39
 
 constexpr int kEdgeSlots = (FT8_LDPC_E + kWave - 1) / kWave;  // 9
 constexpr int kVarSlots = (FT8_LDPC_N + kWave - 1) / kWave;   // 3
@@ -495,6 +495,52 @@ __device__ void extract_llr(const BpArgs& a, const T* wf, int at, int af, double
   }
 }
 
+// The same with the gathers spread over the wave: lane 8 g + i fetches tone i of symbol 8 r + g in
+// round r, so one load instruction covers 8 symbols' rows (one or two cache lines each) instead of
+// 58 rows -- a candidate costs ~8x fewer L1 tag lookups -- and the tone powers reach their symbol's
+// lane through LDS (stage: 64 symbols x 8 tones).
+template <typename T>
+__device__ void extract_llr_coop(const BpArgs& a, const T* wf, int at, int af, double* c, T* stage, int lane) {
+  const int i = lane & 7, g = lane >> 3;
+  const int base = floordiv(at, a.sps);
+  T v[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    const int k = 8 * r + g;
+    const int sym = k + (k < 29 ? 7 : 14);
+    const int block = base + sym;
+    v[r] = (T)0;
+    if (k < 58 && !(block < 0 || block >= a.num_blocks))
+      v[r] = wf[(int64_t)(at + sym * a.sps) * a.F + af + i * a.bpt];
+  }
+#pragma unroll
+  for (int r = 0; r < 8; ++r) stage[8 * (8 * r + g) + i] = v[r];
+  __syncthreads();
+  if (lane < 58) {
+    const int k = lane;
+    const int sym = k + (k < 29 ? 7 : 14);
+    const int block = base + sym;
+    double l0 = 0.0, l1 = 0.0, l2 = 0.0;
+    if (!(block < 0 || block >= a.num_blocks)) {
+      double s[8], s2[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s[j] = (double)stage[8 * k + j];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s2[j] = s[kGrayD[j]];
+      l0 = pymax4(s2[4], s2[5], s2[6], s2[7]) - pymax4(s2[0], s2[1], s2[2], s2[3]);
+      l1 = pymax4(s2[2], s2[3], s2[6], s2[7]) - pymax4(s2[0], s2[1], s2[4], s2[5]);
+      l2 = pymax4(s2[1], s2[3], s2[5], s2[7]) - pymax4(s2[0], s2[2], s2[4], s2[6]);
+    }
+    c[3 * k] = l0;
+    c[3 * k + 1] = l1;
+    c[3 * k + 2] = l2;
+  }
+}
+
+#ifndef LLR_COOP
+#define LLR_COOP 1
+#endif
+
 // ---- k_llr: one wave per candidate -> normalised LLRs in global memory ---------------------------
 // modes: 0 per-slot candidate lists (skips ranks >= the slot's count), 1 explicit (slot, t, f) list,
 // 2 normalise given LLRs
@@ -531,7 +577,12 @@ __global__ __launch_bounds__(kWave) void k_llr(BpArgs a) {
   if (a.mode == 2) {
     for (int n = lane; n < FT8_LDPC_N; n += kWave) c[n] = a.llr_in[(int64_t)item * FT8_LDPC_N + n];
   } else {
+#if LLR_COOP
+    __shared__ T stage[64 * 8];
+    extract_llr_coop<T>(a, reinterpret_cast<const T*>(a.wf) + (int64_t)slot * a.T * a.F, at, af, c, stage, lane);
+#else
     extract_llr<T>(a, reinterpret_cast<const T*>(a.wf) + (int64_t)slot * a.T * a.F, at, af, c, lane);
+#endif
   }
   __syncthreads();
   if (a.normalize) {  // ftx_normalize_logl (ft8_decode.py:190-198)
