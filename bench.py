@@ -517,6 +517,17 @@ def main():
         if st == "bp":
             cn = ctx.counters(reset=True)
     ctx.set_timing(False, stages=None)
+    # the STFT is the first kernel of a step, so an event placed before it also times the host's
+    # launch gap; its launch duration comes from back-to-back re-launches of the step's STFT instead
+    # (ft8_replay_stage), events only around the whole run
+    stft_reps = 20
+    ctx.replay("stft", 2)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    ctx.replay("stft", stft_reps)
+    e1.record()
+    torch.cuda.synchronize()
+    stft_replay_ms = e0.elapsed_time(e1) / stft_reps
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -533,7 +544,7 @@ def main():
     value = total_slots / elapsed
     K = args.steps
     bp_ms = stage_ms["bp"]
-    stft_ms = stage_ms["stft"]
+    stft_ms = stft_replay_ms
     # dominant kernel: k_bp.  Algorithmic FLOPs per launch from the device counters.
     f_pass = bp_flops_per_pass()
     f_hd = 174 * 3
@@ -619,7 +630,9 @@ def main():
         "roofline_hbm": {"kernel": "k_stft", "bound": "hbm", "achieved": stft_gbs, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": stft_gbs / HBM_PEAK_GBS,
                          "traffic": hbm("ft8::k_stft"), "traffic_source": tsrc,
-                         "bytes_per_launch": stft_bytes, "launch_ms": stft_ms},
+                         "bytes_per_launch": stft_bytes, "launch_ms": stft_ms,
+                         "launch_ms_from": f"{stft_reps} back-to-back re-launches of the step's STFT "
+                                           "(ft8_replay_stage), HIP events around the run"},
         "stages_ms": stage_ms,
         "stages_sum_ms": sum(stage_ms.values()),
         "bp_stress": stress,
