@@ -50,8 +50,20 @@ constexpr int kProdGroup = BP_PROD_GROUP;
 #ifndef BP_WAVES_PER_EU
 #define BP_WAVES_PER_EU 4
 #endif
-#ifndef BP_FOLD_HALF
-#define BP_FOLD_HALF 1  // fast_tanh's -1/2 argument scaling folded into its polynomial constants
+// The register budget the compiler is given: at a 4-wave budget (128 VGPRs) the allocator spills
+// ~50 VGPRs of the fused sweep to scratch, although under a 3-wave budget it needs only 118 -- which
+// still leaves 4 waves resident per SIMD (512 / 120), the residency the grid is sized for.
+#ifndef BP_LB_WAVES
+#define BP_LB_WAVES 3
+#endif
+#ifndef BP_SKIP_LAST
+#define BP_SKIP_LAST 1  // the last iteration's (unread) message update is not computed
+#endif
+#ifndef BP_FUSE_AC
+#define BP_FUSE_AC 1  // fast_tanh in phase A's variable-major order, from registers (no LDS round trip)
+#endif
+#ifndef BP_FIRST_SWEEP
+#define BP_FIRST_SWEEP 1  // first sweep (all tov 0): one fast_tanh per variable instead of per edge
 #endif
 [[maybe_unused]] constexpr double kClip2 = 2.0 * 4.97;  // exact: twice fast_tanh's clip bound
 #ifndef BP_GRID_CUS
@@ -232,18 +244,11 @@ static_assert(offsetof(WaveLds, msg) == kHdr, "msg follows the header");
 
 // Per-lane tables (registers, built once per wave).
 //   va[j], vb[j]: variable n = lane + 64 j (variable-major phase): LDS byte addresses of its three
-//                 edge messages in the reference's kFTX_LDPC_Mn order (va: 1st | 2nd << 16, vb: 3rd)
+//                 edge messages in the reference's kFTX_LDPC_Mn order (va, va1, vb)
 //   h[k][j]:      check m' = lane + 64 k (parity): its variables as a 174-bit mask, 64-bit word j
 //                 (lo, hi) -- the parity is popcount(h & hard decisions) from wave ballots
-#ifndef BP_VA_FULL
-#define BP_VA_FULL 1  // full addresses: no extraction ops in phase A (110 VGPRs; 0 = packed 16-bit pairs)
-#endif
 struct WaveTables {
-#if BP_VA_FULL
   uint32_t va[kVarSlots], va1[kVarSlots];
-#else
-  uint32_t va[kVarSlots];
-#endif
   uint32_t vb[kVarSlots];
   uint32_t h[kChkSlots][kVarSlots][2];
 };
@@ -277,20 +282,12 @@ __device__ void load_tables(WaveTables& t, WaveLds& L, int lane) {
   for (int j = 0; j < kVarSlots; ++j) {
     const int n = lane + kWave * j;
     if (n < FT8_LDPC_N) {
-#if BP_VA_FULL
       t.va[j] = addr_of(kVarEdgeD[3 * n]);
       t.va1[j] = addr_of(kVarEdgeD[3 * n + 1]);
-#else
-      t.va[j] = addr_of(kVarEdgeD[3 * n]) | (addr_of(kVarEdgeD[3 * n + 1]) << 16);
-#endif
       t.vb[j] = addr_of(kVarEdgeD[3 * n + 2]);
     } else {  // padding variable: reads the constant, never stores (see the sweep)
       const uint32_t one = msg0 + 8u * kOne;
-#if BP_VA_FULL
       t.va[j] = t.va1[j] = one;
-#else
-      t.va[j] = one | (one << 16);
-#endif
       t.vb[j] = one;
     }
   }
@@ -316,10 +313,8 @@ __device__ void load_tables(WaveTables& t, WaveLds& L, int lane) {
   // keep the tables in registers: opaque values cannot be rematerialised from memory in the loop
 #pragma unroll
   for (int j = 0; j < kVarSlots; ++j) asm volatile("" : "+v"(t.va[j]), "+v"(t.vb[j]));
-#if BP_VA_FULL
 #pragma unroll
   for (int j = 0; j < kVarSlots; ++j) asm volatile("" : "+v"(t.va1[j]));
-#endif
 #pragma unroll
   for (int k = 0; k < kChkSlots; ++k)
 #pragma unroll
@@ -614,9 +609,82 @@ __device__ __forceinline__ void sweep_sync() {
 #endif
 }
 
+// fast_tanh (ldpc_decoder.py:11-20) of kDivGroup clipped arguments in place: y = clip(T, +-2 c) in,
+// toc out (see the sweep's phase C for the scaling argument)
+__device__ __forceinline__ void tanh_group(double* v) {
+  double na[kDivGroup], nb[kDivGroup];
+  double mn = INFINITY;
+#pragma unroll
+  for (int i = 0; i < kDivGroup; ++i) {
+    const double yv = v[i], z = yv * yv;
+    na[i] = yv * (15120.0 + z * (420.0 + z));
+    nb[i] = -30240.0 + z * (-3360.0 + z * -30.0);
+    mn = __builtin_fmin(mn, __builtin_fabs(na[i]));
+  }
+  if (__ballot(mn >= 0x1p-480) == __builtin_amdgcn_read_exec()) {
+    div_fast<kDivGroup>(v, na, nb);
+  } else {
+#pragma unroll
+    for (int i = 0; i < kDivGroup; ++i) {
+      const double xv = -0.5 * v[i], x2 = xv * xv;
+      na[i] = xv * (945.0 + x2 * (105.0 + x2));
+      nb[i] = 945.0 + x2 * (420.0 + x2 * 15.0);
+    }
+    div_rn<kDivGroup>(v, na, nb);
+  }
+}
+
+// tov = -2 fast_atanh(Tmn) (ldpc_decoder.py:22-30, 108) of kDivGroup products in place.
+__device__ __forceinline__ void atanh_group(double* v) {
+  double na[kDivGroup], nb[kDivGroup];
+#pragma unroll
+  for (int i = 0; i < kDivGroup; ++i) {
+    const double xv = v[i], x2 = xv * xv;
+    na[i] = xv * (945.0 + x2 * (-735.0 + x2 * 64.0));
+    // -b/2 for b = 945 + x2 (-1050 + x2 225): every step is the reference's step scaled by -1/2,
+    // exact (terms too small to scale exactly are absorbed by the constant they meet)
+    nb[i] = (-472.5 + x2 * (525.0 + x2 * -112.5));
+  }
+  div_rn<kDivGroup, true>(v, na, nb);
+}
+
+// Phase D's products: for each of the lane's edge slots, the product of the other toc of the edge's
+// check in row order, from 1.0 (1.0 * t0 == t0, so the product starts at the first factor).
+__device__ __forceinline__ void check_products(double* x, uint32_t la, int lane) {
+#pragma unroll
+  for (int i = 0; i < kEdgeSlots; ++i) {
+    const int qa = qa_of(i);
+    const bool mx = mixed_slot(i);
+    const bool hi = mx && lane >= hi_lane(i);
+    // row base of the lane (factor 0 of its row): la + row_off(i) for q = qa, 664 less for qa + 1
+    const uint32_t rb = hi ? la - 664u : la;
+    double p = 0.0;
+    bool first = true;
+#pragma unroll
+    for (int f = 0; f < 7; ++f) {
+      double t;
+      if (mx && f == qa) {        // t[qa + 1] (q = qa lanes) or t[qa] (q = qa + 1 lanes)
+        const uint32_t pa = hi ? rb : rb + 664u;
+        t = ldv(pa + (uint32_t)(row_off(i) + 664 * qa));
+      } else if (mx && f == qa + 1) {
+        continue;
+      } else if (!mx && f == qa) {
+        continue;
+      } else {
+        t = ldv(rb + (uint32_t)(row_off(i) + 664 * f));
+      }
+      p = first ? t : p * t;
+      first = false;
+    }
+    x[i] = p;
+    // bound how far the scheduler hoists these loads (register pressure)
+    if (i % kProdGroup == kProdGroup - 1) asm volatile("" ::: "memory");
+  }
+}
+
 // ---- k_bp: persistent waves, one candidate at a time ----------------------------------------------
 // modes: 0 per-slot candidate lists (records carry slot / abs_time / abs_freq / score), 2 plain LLRs
-__global__ __launch_bounds__(kWave, BP_WAVES_PER_EU) void k_bp(BpArgs a) {
+__global__ __launch_bounds__(kWave, BP_LB_WAVES) void k_bp(BpArgs a) {
   __shared__ WaveLds L;
   const int lane = threadIdx.x;
   WaveTables tb;
@@ -659,9 +727,11 @@ __global__ __launch_bounds__(kWave, BP_WAVES_PER_EU) void k_bp(BpArgs a) {
     // ---- belief propagation (ldpc_decoder.py:54-113) ----------------------------------------
     // One sweep = the reference iteration.  (A) variable-major: each lane reads its variables'
     // three tov, forms the hard decision c + ((t0 + t1) + t2) (a wave ballot per variable slot)
-    // and the three variable->check sums (c + t_a) + t_b, and writes the clipped -T/2 into each
-    // edge's slot; (B) parity of every check from the ballots; (C) edge-major: fast_tanh -> toc;
-    // (D) check products -> fast_atanh -> tov.
+    // and the three clipped variable->check sums (c + t_a) + t_b in registers; (B) parity of every
+    // check from the ballots; (C) fast_tanh of those registers, a variable's three edges being one
+    // division group, toc stored into each edge's slot; (D) edge-major: check products ->
+    // fast_atanh -> tov.  The first sweep (all tov 0) evaluates fast_tanh once per variable; the
+    // last one stops after (B), its message update being unread.
     // tov = 0 on every real edge (indices 0..521; the constants above never change)
 #pragma unroll
     for (int i = 0; i < kEdgeSlots; ++i)
@@ -677,14 +747,46 @@ __global__ __launch_bounds__(kWave, BP_WAVES_PER_EU) void k_bp(BpArgs a) {
       // the loop (spilling); recomputing them is one integer op each
 #pragma unroll
       for (int j = 0; j < kVarSlots; ++j) asm volatile("" : "+v"(tb.va[j]), "+v"(tb.vb[j]));
+#if BP_FUSE_AC
+      // (A) variable-major: the hard decision and the three clipped variable->check arguments of
+      // each of the lane's variables, kept in registers (no LDS store, so no phase boundary)
+      double y[kVarSlots][3];
+      const bool sweep0 = BP_FIRST_SWEEP && iter == 0;
+      if (sweep0) {
+        // every tov is 0: messages = codeword + 0.0 (ldpc_decoder.py:72-73), and the argument of
+        // each of a variable's edges is (c + 0.0) + 0.0 == c + 0.0
+#pragma unroll
+        for (int j = 0; j < kVarSlots; ++j) {
+          const double T = cv_[j] + 0.0;
+          hd[j] = __ballot(T > 0.0);
+          y[j][0] = y[j][1] = y[j][2] = __builtin_fmin(__builtin_fmax(T, -kClip2), kClip2);
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < kVarSlots; ++j) {
+          const double t0 = *(lds_f64*)(uintptr_t)tb.va[j];
+          const double t1 = *(lds_f64*)(uintptr_t)tb.va1[j];
+          const double t2 = *(lds_f64*)(uintptr_t)tb.vb[j];
+          const double c = cv_[j];
+          // messages = codeword + sum(tov, axis=1) (ldpc_decoder.py:72-73)
+          hd[j] = __ballot((c + ((t0 + t1) + t2)) > 0.0);
+          // Tnm = codeword[n] + the other two tov in check order (ldpc_decoder.py:90-96); fast_tanh's
+          // np.clip with the -1/2 folded into the polynomials: y = clip(T, -2 c, 2 c) (no NaN here)
+          const double c0 = c + t0;
+          y[j][0] = __builtin_fmin(__builtin_fmax((c + t1) + t2, -kClip2), kClip2);
+          y[j][1] = __builtin_fmin(__builtin_fmax(c0 + t2, -kClip2), kClip2);
+          y[j][2] = __builtin_fmin(__builtin_fmax(c0 + t1, -kClip2), kClip2);
+        }
+      }
+      // padding variables (slot 2, lanes >= 46) evaluate a harmless 1.0 so that their wave stays on
+      // the short division, and store nothing
+      if (!var2) y[kVarSlots - 1][0] = y[kVarSlots - 1][1] = y[kVarSlots - 1][2] = 1.0;
+      hd[kVarSlots - 1] &= var2_mask;
+#else
       // (A) hard decision + variable -> check arguments
 #pragma unroll
       for (int j = 0; j < kVarSlots; ++j) {
-#if BP_VA_FULL
         const uint32_t a0 = tb.va[j], a1 = tb.va1[j], a2 = tb.vb[j];
-#else
-        const uint32_t a0 = tb.va[j] & 0xFFFFu, a1 = tb.va[j] >> 16, a2 = tb.vb[j];
-#endif
         const double t0 = *(lds_f64*)(uintptr_t)a0;
         const double t1 = *(lds_f64*)(uintptr_t)a1;
         const double t2 = *(lds_f64*)(uintptr_t)a2;
@@ -696,20 +798,15 @@ __global__ __launch_bounds__(kWave, BP_WAVES_PER_EU) void k_bp(BpArgs a) {
         const double T0 = (c + t1) + t2, T1 = c0 + t2, T2 = c0 + t1;
         // fast_tanh's np.clip (no NaN reaches here)
         if (j < kVarSlots - 1 || var2) {
-#if BP_FOLD_HALF
           // y = clip(T, -2 c, 2 c) = -2 clip(-T / 2, -c, c), c = 4.97: the -1/2 goes into phase C
           *(__attribute__((address_space(3))) double*)(uintptr_t)a0 = __builtin_fmin(__builtin_fmax(T0, -kClip2), kClip2);
           *(__attribute__((address_space(3))) double*)(uintptr_t)a1 = __builtin_fmin(__builtin_fmax(T1, -kClip2), kClip2);
           *(__attribute__((address_space(3))) double*)(uintptr_t)a2 = __builtin_fmin(__builtin_fmax(T2, -kClip2), kClip2);
-#else
-          *(__attribute__((address_space(3))) double*)(uintptr_t)a0 = __builtin_fmin(__builtin_fmax(-T0 / 2, -4.97), 4.97);
-          *(__attribute__((address_space(3))) double*)(uintptr_t)a1 = __builtin_fmin(__builtin_fmax(-T1 / 2, -4.97), 4.97);
-          *(__attribute__((address_space(3))) double*)(uintptr_t)a2 = __builtin_fmin(__builtin_fmax(-T2 / 2, -4.97), 4.97);
-#endif
         }
       }
       hd[kVarSlots - 1] &= var2_mask;
       sweep_sync();
+#endif
       // all-zero hard decision -> stop (ldpc_decoder.py:76-78)
       if ((hd[0] | hd[1] | hd[2]) == 0) break;
       // (B) parity check (ldpc_check, ldpc_decoder.py:33-52): popcount of (row mask & decisions)
@@ -728,104 +825,55 @@ __global__ __launch_bounds__(kWave, BP_WAVES_PER_EU) void k_bp(BpArgs a) {
         min_errors = errs;
         if (errs == 0) break;
       }
-      double x[kEdgeSlots];
-#pragma unroll
-      for (int i = 0; i < kEdgeSlots; ++i) x[i] = *(lds_f64*)(uintptr_t)(la + 512u * i);
-      // variable -> check messages: toc = fast_tanh(-Tnm / 2), three interleaved divisions at a time
-#if BP_FOLD_HALF
-      // From y = -2 x (x the reference's clipped argument): with z = RN(y y) = 4 RN(x x), every step
-      // of fast_tanh's polynomials (ldpc_decoder.py:11-20) is the reference's step scaled by a power
-      // of two, so na = -A / 32 and nb = B / -32 exactly for
+      // the last iteration's message update (ldpc_decoder.py:88-108) is never read: the loop ends
+      // after it and the result is the plain / min_errors formed above
+      if (BP_SKIP_LAST && iter + 1 == a.max_iterations) break;
+      // (C) variable -> check messages: toc = fast_tanh(-Tnm / 2), three interleaved divisions at a
+      // time.  From y = -2 x (x the reference's clipped argument): with z = RN(y y) = 4 RN(x x),
+      // every step of fast_tanh's polynomials (ldpc_decoder.py:11-20) is the reference's step scaled
+      // by a power of two, so na = -A / 32 and nb = B / -32 exactly for
       //   A = y (15120 + z (420 + z)),   B = -30240 + z (-3360 + z (-30)),
       // and toc = RN(na / nb) = RN(A / B): the same real quotient.  The scalings are exact while
       // nothing underflows, which |A| >= 2^-480 (so |y| >= 2^-496) guarantees for the whole wave;
       // the same bound admits the short division.  Otherwise (tiny or zero arguments) the group
-      // runs the reference form on x = -y / 2.
+      // runs the reference form on x = -y / 2 (tanh_group).
+#if BP_FUSE_AC
+      // variable-major, straight from phase A's registers into each edge's slot
+      static_assert(kDivGroup == 3 && kVarSlots == 3, "a division group is one variable's edges");
+      if (sweep0) {  // one fast_tanh per variable
+        double v[kVarSlots] = {y[0][0], y[1][0], y[2][0]};
+        tanh_group(v);
 #pragma unroll
-      for (int g = 0; g < kEdgeSlots; g += kDivGroup) {
-        double na[kDivGroup], nb[kDivGroup];
-        double mn = INFINITY;
-#pragma unroll
-        for (int i = 0; i < kDivGroup; ++i) {
-          const double yv = x[g + i], z = yv * yv;
-          na[i] = yv * (15120.0 + z * (420.0 + z));
-          nb[i] = -30240.0 + z * (-3360.0 + z * -30.0);
-          mn = __builtin_fmin(mn, __builtin_fabs(na[i]));
-        }
-        if (__ballot(mn >= 0x1p-480) == __builtin_amdgcn_read_exec()) {
-          div_fast<kDivGroup>(&x[g], na, nb);
-        } else {
-#pragma unroll
-          for (int i = 0; i < kDivGroup; ++i) {
-            const double xv = -0.5 * x[g + i], x2 = xv * xv;
-            na[i] = xv * (945.0 + x2 * (105.0 + x2));
-            nb[i] = 945.0 + x2 * (420.0 + x2 * 15.0);
-          }
-          div_rn<kDivGroup>(&x[g], na, nb);
-        }
+        for (int j = 0; j < kVarSlots; ++j) y[j][0] = y[j][1] = y[j][2] = v[j];
       }
+#pragma unroll
+      for (int j = 0; j < kVarSlots; ++j) {
+        if (!sweep0) tanh_group(y[j]);
+        if (j < kVarSlots - 1 || var2) {
+          *(__attribute__((address_space(3))) double*)(uintptr_t)tb.va[j] = y[j][0];
+          *(__attribute__((address_space(3))) double*)(uintptr_t)tb.va1[j] = y[j][1];
+          *(__attribute__((address_space(3))) double*)(uintptr_t)tb.vb[j] = y[j][2];
+        }
+        asm volatile("" ::: "memory");  // one group's temporaries at a time (register pressure)
+      }
+      sweep_sync();
+      double x[kEdgeSlots];
 #else
+      double x[kEdgeSlots];
 #pragma unroll
-      for (int g = 0; g < kEdgeSlots; g += kDivGroup) {
-        double na[kDivGroup], nb[kDivGroup];
+      for (int i = 0; i < kEdgeSlots; ++i) x[i] = *(lds_f64*)(uintptr_t)(la + 512u * i);
 #pragma unroll
-        for (int i = 0; i < kDivGroup; ++i) {
-          const double xv = x[g + i], x2 = xv * xv;
-          na[i] = xv * (945.0 + x2 * (105.0 + x2));
-          nb[i] = 945.0 + x2 * (420.0 + x2 * 15.0);
-        }
-        div_rn<kDivGroup>(&x[g], na, nb);
-      }
-#endif
+      for (int g = 0; g < kEdgeSlots; g += kDivGroup) tanh_group(&x[g]);
 #pragma unroll
       for (int i = 0; i < kEdgeSlots; ++i)
         if (i < kEdgeSlots - 1 || lane + kWave * i < FT8_LDPC_E)
           *(__attribute__((address_space(3))) double*)(uintptr_t)(la + 512u * i) = x[i];
       sweep_sync();
-      // check -> variable messages: tov = -2 fast_atanh(prod of the other toc of the check, in row
-      // order, from 1.0; 1.0 * t0 == t0, so the product starts at the first factor)
+#endif
+      // (D) check -> variable messages: tov = -2 fast_atanh(product of the other toc of the check)
+      check_products(x, la, lane);
 #pragma unroll
-      for (int i = 0; i < kEdgeSlots; ++i) {
-        const int qa = qa_of(i);
-        const bool mx = mixed_slot(i);
-        const bool hi = mx && lane >= hi_lane(i);
-        // row base of the lane (factor 0 of its row): la + row_off(i) for q = qa, 664 less for qa + 1
-        const uint32_t rb = hi ? la - 664u : la;
-        double p = 0.0;
-        bool first = true;
-#pragma unroll
-        for (int f = 0; f < 7; ++f) {
-          double t;
-          if (mx && f == qa) {        // t[qa + 1] (q = qa lanes) or t[qa] (q = qa + 1 lanes)
-            const uint32_t pa = hi ? rb : rb + 664u;
-            t = ldv(pa + (uint32_t)(row_off(i) + 664 * qa));
-          } else if (mx && f == qa + 1) {
-            continue;
-          } else if (!mx && f == qa) {
-            continue;
-          } else {
-            t = ldv(rb + (uint32_t)(row_off(i) + 664 * f));
-          }
-          p = first ? t : p * t;
-          first = false;
-        }
-        x[i] = p;
-        // bound how far the scheduler hoists these loads (register pressure)
-        if (i % kProdGroup == kProdGroup - 1) asm volatile("" ::: "memory");
-      }
-#pragma unroll
-      for (int g = 0; g < kEdgeSlots; g += kDivGroup) {
-        double na[kDivGroup], nb[kDivGroup];
-#pragma unroll
-        for (int i = 0; i < kDivGroup; ++i) {
-          const double xv = x[g + i], x2 = xv * xv;
-          na[i] = xv * (945.0 + x2 * (-735.0 + x2 * 64.0));
-          // -b/2 for b = 945 + x2 (-1050 + x2 225): every step is the reference's step scaled by
-          // -1/2, exact (terms too small to scale exactly are absorbed by the constant they meet)
-          nb[i] = (-472.5 + x2 * (525.0 + x2 * -112.5));
-        }
-        div_rn<kDivGroup, true>(&x[g], na, nb);  // tov = -2 fast_atanh(Tmn)
-      }
+      for (int g = 0; g < kEdgeSlots; g += kDivGroup) atanh_group(&x[g]);
 #pragma unroll
       for (int i = 0; i < kEdgeSlots; ++i)
         if (i < kEdgeSlots - 1 || lane + kWave * i < FT8_LDPC_E)
