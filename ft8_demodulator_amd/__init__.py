@@ -4,7 +4,7 @@ Public API mirrors the reference's ft8_demodulator package (src/ft8_tools/ft8_de
 decode_ft8_message, calculate_spectrogram, select_frequency_band,
 create_waterfall_from_spectrogram, ft8_find_candidates, ft8_decode_candidate, bp_decode,
 ldpc_check, compute_crc/extract_crc/add_crc and the FT8* dataclasses -- plus the WAV entry
-point (from_wave) and a batched slot decoder (batch.decode_slots).  Every numeric stage runs in
+point (from_wave) and a batched slot decoder (SlotDecoder, decode_slots).  Every numeric stage runs in
 hand-written HIP kernels (csrc/) reached through the C-ABI library libft8hip.so; there is no
 CPU fallback: calls fail loudly when the library or a GPU is missing.
 """
@@ -18,4 +18,4 @@ from .ft8_decode import (  # noqa: E402,F401
 from .ldpc_decoder import bp_decode, ldpc_check  # noqa: E402,F401
 from .crc import add_crc, compute_crc, extract_crc  # noqa: E402,F401
 from .from_wave import decode_ft8_from_wave, read_wave_file  # noqa: E402,F401
-from ._pipeline import SlotDecoder  # noqa: E402,F401
+from ._pipeline import SlotDecoder, decode_slots  # noqa: E402,F401

@@ -259,3 +259,9 @@ class SlotDecoder:
 
     def timing(self, reset=False):
         return self.ctx.timing(reset)
+
+
+def decode_slots(samples, sample_rate=12000, **kwargs):
+    """One-call form of SlotDecoder: samples [B, N] (GPU tensor, float32/int16/...) -> list (per
+    slot) of decode_ft8_message's 5-tuples."""
+    return SlotDecoder(sample_rate=sample_rate, **kwargs).decode(samples)

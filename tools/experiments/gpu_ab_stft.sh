@@ -1,5 +1,5 @@
 # STFT A/B: STFT + e2e parity tests on the candidate variants, then interleaved timing rounds.
-# usage: TESTED="P" bash tools/gpu_ab_stft.sh TAG O P
+# usage: TESTED="P" bash tools/experiments/gpu_ab_stft.sh TAG O P
 set -o pipefail
 T=$1; shift
 mkdir -p gpurun_out

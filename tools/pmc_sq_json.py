@@ -1,4 +1,4 @@
-"""SQ/GRBM counter pass (tools/gpu_pmc_all.sh) -> profiles/<name>.json: per kernel, the last dispatch's
+"""SQ/GRBM counter pass (tools/experiments/gpu_pmc_all.sh) -> profiles/<name>.json: per kernel, the last dispatch's
 counters plus derived fractions.  SQ_WAVE_CYCLES / SQ_WAIT_* / SQ_ACTIVE_INST_* count quad-cycles
 summed over waves; GRBM_GUI_ACTIVE counts cycles summed over the 8 XCDs (MI355X_MICROARCH.md), so
 
