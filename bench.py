@@ -388,7 +388,7 @@ def launch_ranks(args):
     import subprocess
     import torch
     n_dev = torch.cuda.device_count()  # does not initialise HIP on this image
-    if n_dev < args.gpus:
+    if n_dev < (1 if args.share_gpu else args.gpus):
         print(f"bench.py: --gpus {args.gpus} requested but only {n_dev} GPU(s) are visible", file=sys.stderr)
         return 2
     with socket.socket() as so:
@@ -416,6 +416,9 @@ def main():
     ap.add_argument("--no-h2d", action="store_true", help="skip the PCIe-inclusive streaming leg")
     ap.add_argument("--no-subtract", action="store_true", help="skip the config-4 subtract-and-redecode leg")
     ap.add_argument("--no-drift", action="store_true", help="skip the frequency-drift correction leg")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="rehearsal of the N > 1 path on a one-GPU box: every rank on cuda:0, gloo instead of "
+                         "RCCL (exercises the launch, sharding and decode gather; not a measurement)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" in os.environ:
@@ -435,7 +438,7 @@ def main():
     import torch.distributed as dist
 
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = 0 if args.share_gpu else int(os.environ.get("LOCAL_RANK", "0"))
     kw = dict(max_candidates=300, min_score=2, max_iterations=20)
     S = args.slots
     seed0 = 100000 + rank * S  # global slot g uses seed 100000 + g
@@ -450,7 +453,10 @@ def main():
     dev = torch.device("cuda", local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=dev)
+        if args.share_gpu:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     from ft8_demodulator_amd import SlotDecoder, synth, _lib
     from ft8_demodulator_amd.distributed import gather_decodes
@@ -599,6 +605,7 @@ def main():
         "value": value,
         "unit": "slots/s",
         "n_gpus": world,
+        **({"rehearsal": "--share-gpu: every rank on cuda:0 over gloo; not a measurement"} if args.share_gpu else {}),
         "steps": K,
         "warmup": args.warmup,
         "ms_per_step": elapsed / K * 1e3,
