@@ -16,11 +16,12 @@
 // This file is built with packed math enabled and FMA contraction (Makefile); the FFT is not
 // pocketfft in either case, and tests bound the dB error (tests/test_gpu_stft.py).
 //
-// Work decomposition (unchanged from the scalar kernel it replaces): 128 threads, one butterfly
-// per thread per stage (stage 2 runs two), ping-pong LDS buffers, twiddles formed in registers by
-// recurrence from per-thread seeds; a workgroup walks a run of consecutive frames of one slot and
-// keeps the raw samples in registers, since a frame's second half is the next frame's first half
-// (each run reads (c + 1) / c of its samples), prefetching the next frame's new samples.
+// Work decomposition: 256 threads (four waves) per frame, one butterfly per thread per stage
+// (stage 1 on 120 threads, stage 2 on 240, stage 3 on 128), ping-pong LDS buffers, twiddles formed
+// in registers by recurrence from per-thread seeds; a workgroup walks a run of consecutive frames
+// of one slot and keeps the raw samples in registers, since a frame's second half is the next
+// frame's first half (each run reads (c + 1) / c of its samples), prefetching the next frame's new
+// samples.
 #include "ft8_internal.h"
 
 namespace ft8 {
@@ -193,7 +194,16 @@ __device__ __forceinline__ f2 load_pair(const InT* x, int64_t n0) {
 }
 
 constexpr int kP = 1920;
-constexpr int kThreads38 = 128;
+#ifndef S38_ONEBUF
+#define S38_ONEBUF 0  // 1: one LDS buffer (every stage loads its inputs, barrier, stores): 16 KB per workgroup
+#endif
+#ifndef S38_THREADS
+#define S38_THREADS 256  // four waves per frame: stage 2 one butterfly per thread, stages 1 and 3 on the
+                         // first 120 / 128 threads, the epilogue on all (128: two waves, two stage-2
+                         // butterflies per thread; 0.185 vs 0.175 ms per 256-slot launch)
+#endif
+constexpr int kThreads38 = S38_THREADS;
+static_assert(kThreads38 == 128 || (kThreads38 == 256 && !S38_ONEBUF), "256 threads: two buffers");
 constexpr int kChunk = 8;  // frames per workgroup (24 workgroups per slot at 186 frames)
 
 struct Args {
@@ -209,9 +219,6 @@ struct Args {
 
 __device__ __forceinline__ int pidx(int i) { return i + (i >> 4); }
 
-#ifndef S38_ONEBUF
-#define S38_ONEBUF 0  // 1: one LDS buffer (every stage loads its inputs, barrier, stores): 16 KB per workgroup
-#endif
 #ifndef S38_WINREG
 #define S38_WINREG 1  // the thread's window values stay in registers (0: reloaded from L1 each frame)
 #endif
@@ -289,7 +296,7 @@ __global__ __launch_bounds__(kThreads38) void k_stft3840p(Args a) {
       for (int k = 0; k < 16; ++k) bufA[pidx(16 * t + k)] = y[k];
     }
     __syncthreads();
-    // stage 2: radix 8, Ns = 16: j in {t, t + 128} (j < 240)
+    // stage 2: radix 8, Ns = 16: j in {t, t + 128} (j < 240); with 256 threads j = t
 #if S38_ONEBUF
     f2 v2[2][8];
 #pragma unroll
@@ -303,7 +310,7 @@ __global__ __launch_bounds__(kThreads38) void k_stft3840p(Args a) {
     __syncthreads();  // every stage-2 input is in registers before the buffer is overwritten
 #endif
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < (kThreads38 == 256 ? 1 : 2); ++h) {
       const int j = t + 128 * h;
       if (j < 240) {
 #if S38_ONEBUF
@@ -329,7 +336,7 @@ __global__ __launch_bounds__(kThreads38) void k_stft3840p(Args a) {
     }
     __syncthreads();
     // stage 3: radix 15, Ns = 128: j = t -> natural order into bufA
-    {
+    if (kThreads38 == 128 || t < 128) {
       f2 v[15], y[15];
 #pragma unroll
       for (int r = 0; r < 15; ++r) v[r] = bufB[S38_BIDX(t + 128 * r)];
