@@ -365,9 +365,10 @@ def h2d_stream(x, steps, kw):
         pass
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    return {"workload": f"{steps} batches of {S} int16 PCM slots handed over in pinned host memory, "
-                        "upload on a copy stream overlapped with the previous batch's decode, results "
-                        "copied back to pinned host memory",
+    return {"workload": f"{steps} batches of {S} int16 PCM slots handed over in pinned host memory "
+                        "(ft8_demodulator_amd.stream.StreamDecoder): batch k+2 uploads on a copy stream "
+                        "while batch k+1 decodes and batch k's results are copied back to pinned host "
+                        "memory and converted to the reference's result tuples",
             "slots_per_s": S * steps / dt, "ms_per_batch": dt / steps * 1e3,
             "h2d_bytes_per_batch": int(pcm.numel() * 2)}
 

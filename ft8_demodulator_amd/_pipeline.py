@@ -155,16 +155,26 @@ def device_samples(wave_data, device=None, int16_is_pcm=False):
 
 def records_to_results(recs: np.ndarray, sample_rate: int, bins_per_tone: int, wf_f64: bool):
     """Device records (ok only, candidate order) -> [(FT8Message, FT8DecodeStatus, time_sec,
-    freq_hz, score)] exactly as decode_ft8_message returns them (ft8_decode.py:383-391)."""
+    freq_hz, score)] exactly as decode_ft8_message returns them (ft8_decode.py:383-391).
+
+    time_sec = abs_time / sample_rate and freq_hz = (abs_freq / bins_per_tone) * 6.25 as Python
+    floats, score as the waterfall dtype's NumPy scalar.  Columns are converted once per call (the
+    per-record work is only the object construction)."""
+    n = len(recs)
+    if n == 0:
+        return []
+    payload = recs["payload"].tobytes()
+    crc_c = recs["crc_calculated"].tolist()
+    crc_e = recs["crc_extracted"].tolist()
+    errs = recs["ldpc_errors"].tolist()
+    tsec = [t / sample_rate for t in recs["abs_time"].tolist()]
+    fhz = [(f / bins_per_tone) * FT8_SYMBOL_FREQ_INTERVAL_HZ for f in recs["abs_freq"].tolist()]
+    sc = recs["score"].astype(np.float64 if wf_f64 else np.float32)
     out = []
-    for r in recs:
-        msg = FT8Message(payload=bytearray(r["payload"].tobytes()), hash=int(r["crc_calculated"]))
-        st = FT8DecodeStatus(ldpc_errors=int(r["ldpc_errors"]), crc_extracted=int(r["crc_extracted"]),
-                             crc_calculated=int(r["crc_calculated"]))
-        time_sec = int(r["abs_time"]) / sample_rate
-        freq_hz = (int(r["abs_freq"]) / bins_per_tone) * FT8_SYMBOL_FREQ_INTERVAL_HZ
-        score = np.float64(r["score"]) if wf_f64 else np.float32(r["score"])
-        out.append((msg, st, time_sec, freq_hz, score))
+    for i in range(n):
+        msg = FT8Message(payload=bytearray(payload[10 * i: 10 * i + 10]), hash=crc_c[i])
+        st = FT8DecodeStatus(ldpc_errors=errs[i], crc_extracted=crc_e[i], crc_calculated=crc_c[i])
+        out.append((msg, st, tsec[i], fhz[i], sc[i]))
     return out
 
 

@@ -2,8 +2,9 @@
 pipelining").
 
 Batches of 15-s slots -- typically 16-bit PCM straight from WAV files -- are staged in pinned host
-memory and uploaded on a dedicated copy stream into one of two device buffers, while the previous
-batch is decoded on the compute stream; results come back through pinned host buffers.  int16 PCM
+memory and uploaded on a dedicated copy stream into one of three device buffers: batch k + 2 uploads
+while batch k + 1 decodes on the compute stream and batch k's results are converted on the host;
+results come back through pinned host buffers.  int16 PCM
 is uploaded as-is (half the PCIe bytes of float32) and scaled by the STFT kernel exactly as
 read_wave_file does (from_wave.py:59-67).
 
@@ -24,7 +25,9 @@ from ._pipeline import SlotDecoder, records_to_results
 
 
 class StreamDecoder:
-    """Double-buffered host -> device upload overlapped with ft8_decode_batch."""
+    """Triple-buffered host -> device upload overlapped with ft8_decode_batch."""
+
+    NBUF = 3
 
     def __init__(self, n_samples: int, sample_rate: int = 12000, max_batch: int = 256, pcm16: bool = True,
                  device=None, **decoder_kw):
@@ -41,13 +44,13 @@ class StreamDecoder:
         self.code = _lib.FT8_I16 if pcm16 else _lib.FT8_F32
         self.copy_stream = torch.cuda.Stream(self.dev)
         self.compute = torch.cuda.current_stream(self.dev)
-        self.dbuf = [torch.empty((self.max_batch, self.n), dtype=self.dtype, device=self.dev) for _ in range(2)]
-        self.hbuf = [torch.empty((self.max_batch, self.n), dtype=self.dtype, pin_memory=True) for _ in range(2)]
-        self.freed = [None, None]   # compute-stream event: decode done with dbuf[i]
+        self.dbuf = [torch.empty((self.max_batch, self.n), dtype=self.dtype, device=self.dev) for _ in range(self.NBUF)]
+        self.hbuf = [torch.empty((self.max_batch, self.n), dtype=self.dtype, pin_memory=True) for _ in range(self.NBUF)]
+        self.freed = [None] * self.NBUF   # compute-stream event: decode done with dbuf[i]
         cap = self.dec.cap * _lib.RESULT_DTYPE.itemsize
-        self.hout = [torch.empty(self.max_batch * cap, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
-        self.hcnt = [torch.empty(self.max_batch, dtype=torch.int32, pin_memory=True) for _ in range(2)]
-        self.ready = [None, None]   # compute-stream event: results copied to hout/hcnt[i]
+        self.hout = [torch.empty(self.max_batch * cap, dtype=torch.uint8, pin_memory=True) for _ in range(self.NBUF)]
+        self.hcnt = [torch.empty(self.max_batch, dtype=torch.int32, pin_memory=True) for _ in range(self.NBUF)]
+        self.ready = [None] * self.NBUF   # compute-stream event: results copied to hout/hcnt[i]
         self.caller_upload = None   # copy-stream event of an in-place upload of a caller's pinned tensor
 
     def _stage(self, i: int, batch) -> int:
@@ -105,29 +108,55 @@ class StreamDecoder:
         self.ready[i].synchronize()
         cap = self.dec.cap
         recs = self.hout[i][: nb * cap * _lib.RESULT_DTYPE.itemsize].numpy().view(_lib.RESULT_DTYPE).reshape(nb, cap)
-        cnt = self.hcnt[i][:nb].numpy()
+        cnt = np.minimum(self.hcnt[i][:nb].numpy(), cap)
         out = [[] for _ in range(nb)]
-        for s in np.flatnonzero(cnt > 0):  # most slots decode nothing: skip them without a copy
-            out[s] = records_to_results(recs[s, : min(int(cnt[s]), cap)].copy(), self.fs, self.bpt, False)
+        # every decode of the batch converted in one call (slot-major, candidate order), then dealt
+        sel = np.arange(cap)[None, :] < cnt[:, None]
+        res = records_to_results(recs[sel], self.fs, self.bpt, False)
+        pos = 0
+        for s in np.flatnonzero(cnt > 0).tolist():
+            c = int(cnt[s])
+            out[s] = res[pos: pos + c]
+            pos += c
         return out
 
     def decode_batches(self, batches: Iterable) -> Iterator[List[list]]:
-        """Yield per-slot results of each batch, in order; batch k+1 uploads while batch k decodes."""
-        pending = None
-        for k, batch in enumerate(batches):
-            i = k % 2
+        """Yield per-slot results of each batch, in order.  Two batches are in flight on the device:
+        when batch k's decode ends, batch k + 1 (already uploaded) decodes while batch k + 2 uploads
+        and batch k's results are converted.  A pinned caller tensor is uploaded in place, and its
+        upload has completed before control returns to the caller (who may refill it)."""
+        it = iter(batches)
+        end = object()
+        launched = []   # (buffer, n_slots), oldest first
+        count = 0
+
+        def start(batch):
+            nonlocal count
+            i = count % self.NBUF
+            count += 1
             self.caller_upload = None
             nb = self._stage(i, batch)
             self._launch(i, nb)
-            if self.caller_upload is not None:
-                # a pinned caller tensor is uploaded in place: wait for that upload (it overlaps the
-                # previous batch's decode) before control returns to the caller, who may refill it
-                self.caller_upload.synchronize()
-            if pending is not None:
-                yield self._collect(*pending)
-            pending = (i, nb)
-        if pending is not None:
-            yield self._collect(*pending)
+            launched.append((i, nb))
+            return self.caller_upload
+
+        for _ in range(self.NBUF - 1):      # prime the pipeline
+            batch = next(it, end)
+            if batch is end:
+                break
+            up = start(batch)
+            if up is not None:
+                up.synchronize()
+        while launched:
+            i, nb = launched[0]
+            self.ready[i].synchronize()     # the oldest batch's decode and result copy are done
+            batch = next(it, end)
+            up = start(batch) if batch is not end else None
+            done = self._collect(i, nb)     # conversion overlaps the new upload
+            launched.pop(0)
+            if up is not None:
+                up.synchronize()
+            yield done
 
 
 def decode_wave_files(paths: List[str], batch: int = 256, device=None, **decoder_kw) -> List[list]:

@@ -136,6 +136,24 @@ def test_bp_random_vs_oracle(gpu, oracle):
             assert np.array_equal(pr, p[i]), (it, i)
 
 
+def test_bp_short_iteration_counts_vs_oracle(gpu, oracle):
+    """max_iterations 0..4: no sweep at all, the first sweep alone (k_bp evaluates fast_tanh once per
+    variable there), and the last sweep that stops after the parity check -- all bit-exact."""
+    from ft8_demodulator_amd import _device, synth
+    rng = np.random.default_rng(321)
+    n = 300
+    llrs = np.empty((n, 174))
+    for i in range(n):
+        bits = synth.codeword_bits(synth.random_payload(rng)).astype(np.float64)
+        llrs[i] = oracle.normalize((2 * bits - 1) + (0.4 + 1.0 * (i % 10) / 9) * rng.standard_normal(174))
+    for it in (0, 1, 2, 3, 4):
+        p, rec = _device.bp(llrs, it)
+        for i in range(n):
+            pr, er = oracle.bp_decode(llrs[i], it)
+            assert er == int(rec[i]["ldpc_errors"]), (it, i)
+            assert np.array_equal(pr, p[i]), (it, i)
+
+
 def test_normalize_random_vs_oracle(gpu, oracle):
     from ft8_demodulator_amd import _device
     rng = np.random.default_rng(5)
