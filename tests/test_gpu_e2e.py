@@ -85,6 +85,29 @@ def test_batch_equals_single_and_oracle(gpu, oracle):
         assert set(p for p, _ in got) <= set(q.hex() for q in truth[s].payloads)
 
 
+def test_long_recording_and_large_batch(gpu, oracle):
+    """Sizes beyond one slot: a 61-s recording (four slots' worth of frames, signals in each) decodes
+    like the oracle; a 1024-slot batch (every grid dimension 4x the bench's) equals per-slot decodes
+    on a sample of its slots."""
+    import torch
+    from ft8_demodulator_amd import SlotDecoder, decode_ft8_message, synth
+    kw = dict(max_candidates=300, min_score=2, max_iterations=20)
+    parts, _ = synth.make_slots(4, 12, seed=4100, device="cpu", snr_db=(-16.0, -8.0))
+    x = np.concatenate([parts.numpy().reshape(-1), np.zeros(12000, np.float32)])   # 61 s
+    got = decode_ft8_message(x, 12000, **kw)
+    ref = oracle.decode_ft8_message(x, 12000, **kw)
+    assert sorted((m.payload.hex(), m.hash, t, f) for m, _s, t, f, _sc in got) == \
+        sorted((p.hex(), h, t, f) for (p, h, _e, _ce, _cc, t, f, _sc) in ref)
+    assert len(got) >= 1   # the reference heap keeps the first K passing candidates in scan (time) order
+    big, _ = synth.make_slots(1024, 20, seed=5000, device="cuda")
+    dec = SlotDecoder(12000, **kw)
+    per_slot = dec.decode(big)
+    for s in (0, 1, 511, 777, 1023):
+        assert _rows(per_slot[s]) == _rows(decode_ft8_message(big[s].cpu().numpy(), 12000, **kw)), s
+    del big
+    torch.cuda.empty_cache()
+
+
 def test_stft_i16_equals_f32(gpu):
     import torch
     from ft8_demodulator_amd import _device, read_wave_file
