@@ -373,6 +373,25 @@ def h2d_stream(x, steps, kw):
             "h2d_bytes_per_batch": int(pcm.numel() * 2)}
 
 
+def single_call(x, calls=50):
+    """The drop-in call itself: decode_ft8_message on one host-memory slot (numpy float32, upload
+    and result conversion included), warm, at the reference's defaults and at config 2's K=300."""
+    from ft8_demodulator_amd import decode_ft8_message
+    import torch
+    slot = x[0].cpu().numpy()
+    out = {"workload": "decode_ft8_message(numpy float32 15-s slot, 12 kHz) called back to back on one slot "
+                       "of the batch (host -> device upload, decode, results as the reference's tuples)"}
+    for name, kw in (("defaults_ms", {}), ("k300_min2_ms", dict(max_candidates=300, min_score=2))):
+        for _ in range(5):
+            decode_ft8_message(slot, 12000, **kw)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(calls):
+            decode_ft8_message(slot, 12000, **kw)
+        out[name] = (time.perf_counter() - t0) / calls * 1e3
+    return out
+
+
 REFERENCE_MEASURED = {
     "value": 1.0 / 30.5, "unit": "slots/s", "cores": 1,
     "what": "the reference's own decode_ft8_message (Python/NumPy/SciPy) on one config-2-like slot (50 signals, "
@@ -574,6 +593,7 @@ def main():
     stream = None
     if world == 1 and not args.no_h2d:
         stream = h2d_stream(x, max(3, min(args.steps, 10)), kw)
+    call = single_call(x) if world == 1 else None
     drift = None
     if world == 1 and not args.no_drift:
         drift = drift_correct(dev)
@@ -645,6 +665,7 @@ def main():
         "stages_sum_ms": sum(stage_ms.values()),
         "bp_stress": stress,
         "h2d_stream": stream,
+        "single_call": call,
         "subtract_redecode": sub,
         "drift_correct": drift,
         "cpu_baseline": cpu,
