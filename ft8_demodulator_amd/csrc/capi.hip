@@ -277,7 +277,8 @@ int get_plan(ft8_ctx* c, int nfft, bool cplx, bool f64, FftPlan* out) {
   e.plan.dft = 0;
   // lengths the LDS Stockham FFT cannot take (a prime factor above 7, odd real nfft, above the
   // compiled limit) fall back to the direct DFT kernel: P = nfft, tw = W_nfft^m
-  if ((!cplx && (nfft % 2)) || P > (cplx ? kMaxFftComplex : kMaxFftReal / 2) || !factor(P, e.plan)) {
+  const int max_p = f64 ? kMaxFftP64 : (cplx ? kMaxFftComplex : kMaxFftReal / 2);
+  if ((!cplx && (nfft % 2)) || P > max_p || !factor(P, e.plan)) {
     if (nfft > kMaxDft) return fail(c, FT8_E_RANGE, "nfft " + std::to_string(nfft) + " exceeds the compiled DFT limit");
     P = nfft;
     e.plan.dft = 1;

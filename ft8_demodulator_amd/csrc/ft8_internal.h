@@ -11,8 +11,12 @@ namespace ft8 {
 
 constexpr int kWave = 64;
 constexpr int kMaxCandidates = 4096;   // LDS-resident selection (k_select)
-constexpr int kMaxFftReal = 16384;     // nfft of the real-input path (half-length FFT <= 8192)
-constexpr int kMaxFftComplex = 8192;   // nfft of the complex-input path
+// LDS FFT limits (one (P + P/16 + 1)-point buffer per frame, 256 threads holding P / 256 values each
+// per stage; larger or non-2/3/5/7 lengths take the direct DFT): float32 P <= 10240 (87 KB), float64
+// P <= 8192 (139 KB)
+constexpr int kMaxFftReal = 20480;     // float32 nfft of the real-input path (half-length FFT <= 10240)
+constexpr int kMaxFftComplex = 10240;  // float32 nfft of the complex-input path
+constexpr int kMaxFftP64 = 8192;       // float64: FFT points P (real nfft <= 16384, complex <= 8192)
 constexpr int kMaxDft = 1 << 18;       // nfft of the direct-DFT fallback (any factorisation)
 constexpr int kMaxDftLds = 150 * 1024; // its windowed frame is staged in LDS
 

@@ -338,7 +338,8 @@ __device__ __forceinline__ bool level_better(CT la, int ia, CT lb, int ib) {
 
 template <typename InT, bool CPLX, typename CT, int MAXV>
 // two resident waves per SIMD for P <= 4096 (the LDS allows two float64 3840-point workgroups per
-// CU; the radix-16/15 stages then fit 256 VGPRs), one for the 8192-point variant
+// CU; the radix-16/15 stages then fit 256 VGPRs), one for the 8192- and 10240-point variants (a
+// 16384-point float32 variant, 64 values per thread, trips a gfx950 code-generation error)
 __global__ __launch_bounds__(kThreads, (MAXV <= 16 ? 2 : 1)) void k_stft(StftArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   cplx<CT>* buf = reinterpret_cast<cplx<CT>*>(smem);
@@ -986,7 +987,12 @@ hipError_t launch_t(const StftLaunch& L, const StftArgs& a, hipStream_t s) {
   // of the P <= 4096 variant, whose radix-15 stage would hold two butterflies per thread
   if (a.P <= kThreads * 15) return go(k_stft<InT, CPLX, CT, 15>);
   if (a.P <= kThreads * 16) return go(k_stft<InT, CPLX, CT, 16>);
-  return go(k_stft<InT, CPLX, CT, 32>);
+  if constexpr (sizeof(CT) == 8) {
+    return go(k_stft<InT, CPLX, CT, 32>);  // float64: P <= 8192 (kMaxFftP64)
+  } else {
+    if (a.P <= kThreads * 32) return go(k_stft<InT, CPLX, CT, 32>);
+    return go(k_stft<InT, CPLX, CT, 40>);  // float32 P <= 10240, e.g. nfft 19200 (12 kHz, bpt 10)
+  }
 }
 
 }  // namespace
