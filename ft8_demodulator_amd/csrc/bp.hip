@@ -59,9 +59,6 @@ constexpr int kProdGroup = BP_PROD_GROUP;
 #ifndef BP_SKIP_LAST
 #define BP_SKIP_LAST 1  // the last iteration's (unread) message update is not computed
 #endif
-#ifndef BP_FUSE_AC
-#define BP_FUSE_AC 1  // fast_tanh in phase A's variable-major order, from registers (no LDS round trip)
-#endif
 #ifndef BP_FIRST_SWEEP
 #define BP_FIRST_SWEEP 1  // first sweep (all tov 0): one fast_tanh per variable instead of per edge
 #endif
@@ -609,6 +606,13 @@ __device__ __forceinline__ void sweep_sync() {
 #endif
 }
 
+// np.clip(T, -2 c, 2 c) of fast_tanh's argument in the folded form (c = 4.97); NaN stays NaN when
+// the candidate has NaN inputs (nan_in, wave-uniform)
+__device__ __forceinline__ double clip2(double T, bool nan_in) {
+  const double y = __builtin_fmin(__builtin_fmax(T, -kClip2), kClip2);
+  return (nan_in && T != T) ? T : y;
+}
+
 // fast_tanh (ldpc_decoder.py:11-20) of kDivGroup clipped arguments in place: y = clip(T, +-2 c) in,
 // toc out (see the sweep's phase C for the scaling argument)
 __device__ __forceinline__ void tanh_group(double* v) {
@@ -684,6 +688,7 @@ __device__ __forceinline__ void check_products(double* x, uint32_t la, int lane)
 
 // ---- k_bp: persistent waves, one candidate at a time ----------------------------------------------
 // modes: 0 per-slot candidate lists (records carry slot / abs_time / abs_freq / score), 2 plain LLRs
+template <bool NANSAFE>
 __global__ __launch_bounds__(kWave, BP_LB_WAVES) void k_bp(BpArgs a) {
   __shared__ WaveLds L;
   const int lane = threadIdx.x;
@@ -724,6 +729,14 @@ __global__ __launch_bounds__(kWave, BP_LB_WAVES) void k_bp(BpArgs a) {
       cv_[j] = n < FT8_LDPC_N ? a.llr_in[(int64_t)item * FT8_LDPC_N + n] : 0.0;
     }
 
+    // NaN LLRs must survive np.clip as NaN; the clip's v_min/v_max would turn them into the bound,
+    // so such a candidate (wave-uniform flag) takes the NaN-preserving form.  NaN arises from
+    // nothing else (every other message is finite), and the decode path's normalised LLRs are
+    // either all NaN (ftx_normalize_logl spreads one NaN to all 174, and the all-zero hard decision
+    // then ends the first sweep exactly as in the reference) or none: only the plain-LLR entry
+    // point (ft8_bp, NANSAFE) needs the test.
+    const bool nan_in = NANSAFE && __ballot(cv_[0] != cv_[0] || cv_[1] != cv_[1] || cv_[2] != cv_[2]) != 0;
+
     // ---- belief propagation (ldpc_decoder.py:54-113) ----------------------------------------
     // One sweep = the reference iteration.  (A) variable-major: each lane reads its variables'
     // three tov, forms the hard decision c + ((t0 + t1) + t2) (a wave ballot per variable slot)
@@ -747,7 +760,6 @@ __global__ __launch_bounds__(kWave, BP_LB_WAVES) void k_bp(BpArgs a) {
       // the loop (spilling); recomputing them is one integer op each
 #pragma unroll
       for (int j = 0; j < kVarSlots; ++j) asm volatile("" : "+v"(tb.va[j]), "+v"(tb.vb[j]));
-#if BP_FUSE_AC
       // (A) variable-major: the hard decision and the three clipped variable->check arguments of
       // each of the lane's variables, kept in registers (no LDS store, so no phase boundary)
       double y[kVarSlots][3];
@@ -759,7 +771,7 @@ __global__ __launch_bounds__(kWave, BP_LB_WAVES) void k_bp(BpArgs a) {
         for (int j = 0; j < kVarSlots; ++j) {
           const double T = cv_[j] + 0.0;
           hd[j] = __ballot(T > 0.0);
-          y[j][0] = y[j][1] = y[j][2] = __builtin_fmin(__builtin_fmax(T, -kClip2), kClip2);
+          y[j][0] = y[j][1] = y[j][2] = clip2(T, nan_in);
         }
       } else {
 #pragma unroll
@@ -773,40 +785,27 @@ __global__ __launch_bounds__(kWave, BP_LB_WAVES) void k_bp(BpArgs a) {
           // Tnm = codeword[n] + the other two tov in check order (ldpc_decoder.py:90-96); fast_tanh's
           // np.clip with the -1/2 folded into the polynomials: y = clip(T, -2 c, 2 c) (no NaN here)
           const double c0 = c + t0;
-          y[j][0] = __builtin_fmin(__builtin_fmax((c + t1) + t2, -kClip2), kClip2);
-          y[j][1] = __builtin_fmin(__builtin_fmax(c0 + t2, -kClip2), kClip2);
-          y[j][2] = __builtin_fmin(__builtin_fmax(c0 + t1, -kClip2), kClip2);
+          y[j][0] = (c + t1) + t2;
+          y[j][1] = c0 + t2;
+          y[j][2] = c0 + t1;
+        }
+        // np.clip, NaN-preserving only for a candidate with NaN inputs (a wave-uniform branch)
+        if (nan_in) {
+#pragma unroll
+          for (int j = 0; j < kVarSlots; ++j)
+#pragma unroll
+            for (int e = 0; e < 3; ++e) y[j][e] = clip2(y[j][e], true);
+        } else {
+#pragma unroll
+          for (int j = 0; j < kVarSlots; ++j)
+#pragma unroll
+            for (int e = 0; e < 3; ++e) y[j][e] = clip2(y[j][e], false);
         }
       }
       // padding variables (slot 2, lanes >= 46) evaluate a harmless 1.0 so that their wave stays on
       // the short division, and store nothing
       if (!var2) y[kVarSlots - 1][0] = y[kVarSlots - 1][1] = y[kVarSlots - 1][2] = 1.0;
       hd[kVarSlots - 1] &= var2_mask;
-#else
-      // (A) hard decision + variable -> check arguments
-#pragma unroll
-      for (int j = 0; j < kVarSlots; ++j) {
-        const uint32_t a0 = tb.va[j], a1 = tb.va1[j], a2 = tb.vb[j];
-        const double t0 = *(lds_f64*)(uintptr_t)a0;
-        const double t1 = *(lds_f64*)(uintptr_t)a1;
-        const double t2 = *(lds_f64*)(uintptr_t)a2;
-        const double c = cv_[j];
-        // messages = codeword + sum(tov, axis=1) (ldpc_decoder.py:72-73)
-        hd[j] = __ballot((c + ((t0 + t1) + t2)) > 0.0);
-        // Tnm = codeword[n] + the other two tov in check order (ldpc_decoder.py:90-96)
-        const double c0 = c + t0;
-        const double T0 = (c + t1) + t2, T1 = c0 + t2, T2 = c0 + t1;
-        // fast_tanh's np.clip (no NaN reaches here)
-        if (j < kVarSlots - 1 || var2) {
-          // y = clip(T, -2 c, 2 c) = -2 clip(-T / 2, -c, c), c = 4.97: the -1/2 goes into phase C
-          *(__attribute__((address_space(3))) double*)(uintptr_t)a0 = __builtin_fmin(__builtin_fmax(T0, -kClip2), kClip2);
-          *(__attribute__((address_space(3))) double*)(uintptr_t)a1 = __builtin_fmin(__builtin_fmax(T1, -kClip2), kClip2);
-          *(__attribute__((address_space(3))) double*)(uintptr_t)a2 = __builtin_fmin(__builtin_fmax(T2, -kClip2), kClip2);
-        }
-      }
-      hd[kVarSlots - 1] &= var2_mask;
-      sweep_sync();
-#endif
       // all-zero hard decision -> stop (ldpc_decoder.py:76-78)
       if ((hd[0] | hd[1] | hd[2]) == 0) break;
       // (B) parity check (ldpc_check, ldpc_decoder.py:33-52): popcount of (row mask & decisions)
@@ -837,7 +836,6 @@ __global__ __launch_bounds__(kWave, BP_LB_WAVES) void k_bp(BpArgs a) {
       // nothing underflows, which |A| >= 2^-480 (so |y| >= 2^-496) guarantees for the whole wave;
       // the same bound admits the short division.  Otherwise (tiny or zero arguments) the group
       // runs the reference form on x = -y / 2 (tanh_group).
-#if BP_FUSE_AC
       // variable-major, straight from phase A's registers into each edge's slot
       static_assert(kDivGroup == 3 && kVarSlots == 3, "a division group is one variable's edges");
       if (sweep0) {  // one fast_tanh per variable
@@ -858,18 +856,6 @@ __global__ __launch_bounds__(kWave, BP_LB_WAVES) void k_bp(BpArgs a) {
       }
       sweep_sync();
       double x[kEdgeSlots];
-#else
-      double x[kEdgeSlots];
-#pragma unroll
-      for (int i = 0; i < kEdgeSlots; ++i) x[i] = *(lds_f64*)(uintptr_t)(la + 512u * i);
-#pragma unroll
-      for (int g = 0; g < kEdgeSlots; g += kDivGroup) tanh_group(&x[g]);
-#pragma unroll
-      for (int i = 0; i < kEdgeSlots; ++i)
-        if (i < kEdgeSlots - 1 || lane + kWave * i < FT8_LDPC_E)
-          *(__attribute__((address_space(3))) double*)(uintptr_t)(la + 512u * i) = x[i];
-      sweep_sync();
-#endif
       // (D) check -> variable messages: tov = -2 fast_atanh(product of the other toc of the check)
       check_products(x, la, lane);
 #pragma unroll
@@ -1057,7 +1043,8 @@ hipError_t launch_bp(const BpLaunch& L, hipStream_t s) {
   if (e != hipSuccess) return e;
   const int per_simd = max(1, min(L.grid_waves, BP_WAVES_PER_EU));
   const int waves = min(L.n_items, BP_GRID_CUS * 4 * per_simd);  // resident waves, persistent
-  hipLaunchKernelGGL(k_bp, dim3(waves), dim3(kWave), 0, s, a);
+  if (L.mode == 0) hipLaunchKernelGGL(k_bp<false>, dim3(waves), dim3(kWave), 0, s, a);
+  else hipLaunchKernelGGL(k_bp<true>, dim3(waves), dim3(kWave), 0, s, a);
   return hipGetLastError();
 }
 

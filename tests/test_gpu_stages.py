@@ -183,7 +183,8 @@ def test_crc_and_check(golden, gpu, oracle):
 
 def test_bp_extreme_inputs_vs_oracle(gpu, oracle):
     """Inputs that drive messages to zero / subnormal / huge values exercise the full IEEE
-    division path (the fast path needs 2^-960 <= |numerator| < 2^900): still bit-exact."""
+    division path (the fast path needs 2^-960 <= |numerator| < 2^900), and NaN / infinite LLRs
+    the NaN-preserving clip: still bit-exact."""
     from ft8_demodulator_amd import _device
     rng = np.random.default_rng(77)
     vecs = []
@@ -197,6 +198,16 @@ def test_bp_extreme_inputs_vs_oracle(gpu, oracle):
     v = rng.standard_normal(174)
     v[:60] = 0.0
     vecs.append(v)
+    # NaN and infinite LLRs (bp_decode accepts any vector): np.clip keeps NaN, so it spreads
+    for pos in ([3], [3, 50, 100, 171], list(range(0, 174, 5))):
+        v = rng.standard_normal(174) * 2.0
+        v[pos] = np.nan
+        vecs.append(v)
+    v = rng.standard_normal(174)
+    v[[7, 8]] = np.inf
+    v[[90]] = -np.inf
+    vecs.append(v)
+    vecs.append(np.full(174, np.nan))
     llrs = np.array(vecs)
     for it in (1, 5, 20, 50):
         p, rec = _device.bp(llrs, it)
