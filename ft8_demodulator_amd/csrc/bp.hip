@@ -783,7 +783,7 @@ __global__ __launch_bounds__(kWave, BP_LB_WAVES) void k_bp(BpArgs a) {
           // messages = codeword + sum(tov, axis=1) (ldpc_decoder.py:72-73)
           hd[j] = __ballot((c + ((t0 + t1) + t2)) > 0.0);
           // Tnm = codeword[n] + the other two tov in check order (ldpc_decoder.py:90-96); fast_tanh's
-          // np.clip with the -1/2 folded into the polynomials: y = clip(T, -2 c, 2 c) (no NaN here)
+          // np.clip with the -1/2 folded into the polynomials: y = clip(T, -2 c, 2 c), below
           const double c0 = c + t0;
           y[j][0] = (c + t1) + t2;
           y[j][1] = c0 + t2;
