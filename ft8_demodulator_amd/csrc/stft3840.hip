@@ -204,7 +204,10 @@ constexpr int kP = 1920;
 #endif
 constexpr int kThreads38 = S38_THREADS;
 static_assert(kThreads38 == 128 || (kThreads38 == 256 && !S38_ONEBUF), "256 threads: two buffers");
-constexpr int kChunk = 8;  // frames per workgroup (24 workgroups per slot at 186 frames)
+#ifndef S38_CHUNK
+#define S38_CHUNK 6  // 6: 0.168-0.171 ms vs 8: 0.172-0.178, 4/5/12/16 no better (profiles/r2_s27/s28_*_ab.log)
+#endif
+constexpr int kChunk = S38_CHUNK;  // frames per workgroup (31 workgroups per slot at 186 frames)
 
 struct Args {
   const void* samples;
