@@ -151,7 +151,7 @@ def test_pipeline_settings_do_not_change_results(gpu):
 
 
 def test_stream_decoder_matches_resident_decode(gpu):
-    """Host PCM batches through the double-buffered upload path == decoding the same int16 slots
+    """Host PCM batches through the triple-buffered upload path == decoding the same int16 slots
     already resident on the GPU (and the per-file WAV helper == decode_ft8_from_wave)."""
     import torch
     from ft8_demodulator_amd import SlotDecoder, synth
