@@ -88,10 +88,49 @@ def decode_ft8_from_wave(wave_path: str, freq_min: float = None, freq_max: float
                               device=device)
 
 
+def _print_results(results):
+    if not results:
+        print("No FT8 messages decoded")
+        return
+    print("\nDecoded FT8 messages:")
+    print("-" * 50)
+    for message, status, time_sec, freq_hz, score in results:
+        print(f"Time: {time_sec:.2f} seconds")
+        print(f"Frequency: {freq_hz:.1f} Hz")
+        print(f"Score: {score:.1f}")
+        print(f"Payload: {message.payload.hex()}")
+        print(f"CRC check: {status.crc_calculated}")
+        print(f"LDPC errors: {status.ldpc_errors}")
+        print("-" * 50)
+
+
+def _decode_many(args):
+    """Several files (build-defined extension of the reference CLI): 16-bit PCM files of one sample
+    rate and length are decoded as batches through the streaming path (stream.decode_wave_files);
+    any other file -- and every file with --correction -- one at a time.  Results per file, in order."""
+    from .stream import decode_wave_files
+    kw = dict(freq_min=args.freq_min, freq_max=args.freq_max, time_min=args.time_min, time_max=args.time_max,
+              bins_per_tone=args.bins_per_tone, steps_per_symbol=args.steps_per_symbol,
+              max_candidates=args.max_candidates, min_score=args.min_score, max_iterations=args.max_iterations)
+    out = [None] * len(args.wave_file)
+    groups = {}
+    for i, path in enumerate(args.wave_file):
+        raw, dt, fs = _read_raw(path)
+        if args.correction or dt != np.int16:
+            out[i] = decode_ft8_from_wave(path, correction=args.correction, **kw)
+        else:
+            groups.setdefault((fs, raw.shape[0]), []).append(i)
+    for idx in groups.values():
+        res = decode_wave_files([args.wave_file[i] for i in idx], **kw)
+        for i, r in zip(idx, res):
+            out[i] = r
+    return out
+
+
 def main(argv=None):
-    """from_wave.py:180-229 (same flags)."""
+    """from_wave.py:180-229 (same flags).  Several wave files may be given (decoded as batches)."""
     parser = argparse.ArgumentParser(description="Decode FT8 signals from a wave file (MI355X GPU path)")
-    parser.add_argument("wave_file", help="input wave file")
+    parser.add_argument("wave_file", nargs="+", help="input wave file(s)")
     parser.add_argument("--freq-min", type=float, help="minimum frequency (Hz)")
     parser.add_argument("--freq-max", type=float, help="maximum frequency (Hz)")
     parser.add_argument("--time-min", type=float, help="minimum time (s)")
@@ -103,27 +142,23 @@ def main(argv=None):
     parser.add_argument("--max-iterations", type=int, default=20)
     parser.add_argument("--correction", type=bool, default=False)
     args = parser.parse_args(argv)
-    if not os.path.exists(args.wave_file):
-        print(f"Error: File {args.wave_file} does not exist")
-        sys.exit(1)
+    for path in args.wave_file:
+        if not os.path.exists(path):
+            print(f"Error: File {path} does not exist")
+            sys.exit(1)
+    if len(args.wave_file) > 1:
+        per_file = _decode_many(args)
+        for path, results in zip(args.wave_file, per_file):
+            print(f"\n== {path}")
+            _print_results(results)
+        return per_file
+    args.wave_file = args.wave_file[0]
     results = decode_ft8_from_wave(args.wave_file, freq_min=args.freq_min, freq_max=args.freq_max,
                                    time_min=args.time_min, time_max=args.time_max,
                                    bins_per_tone=args.bins_per_tone, steps_per_symbol=args.steps_per_symbol,
                                    max_candidates=args.max_candidates, min_score=args.min_score,
                                    max_iterations=args.max_iterations, correction=args.correction)
-    if not results:
-        print("No FT8 messages decoded")
-        return results
-    print("\nDecoded FT8 messages:")
-    print("-" * 50)
-    for message, status, time_sec, freq_hz, score in results:
-        print(f"Time: {time_sec:.2f} seconds")
-        print(f"Frequency: {freq_hz:.1f} Hz")
-        print(f"Score: {score:.1f}")
-        print(f"Payload: {message.payload.hex()}")
-        print(f"CRC check: {status.crc_calculated}")
-        print(f"LDPC errors: {status.ldpc_errors}")
-        print("-" * 50)
+    _print_results(results)
     return results
 
 

@@ -108,6 +108,22 @@ def test_long_recording_and_large_batch(gpu, oracle):
     torch.cuda.empty_cache()
 
 
+def test_cli_several_files_equals_one_at_a_time(gpu, capsys):
+    """The WAV CLI with several files (equal-length 16-bit PCM ones batched through the stream path,
+    the 20-kHz one on its own) returns, per file, what the one-file call returns."""
+    from ft8_demodulator_amd import decode_ft8_from_wave
+    from ft8_demodulator_amd.from_wave import main
+    files = [os.path.join(DATA, f) for f in ("synth_cfg1.wav", "ft8_fs20k_f0_550_id_1.wav", "synth_few.wav",
+                                             "synth_cfg2.wav")]
+    per_file = main(files + ["--max-candidates", "300", "--min-score", "2"])
+    assert len(per_file) == len(files)
+    for path, got in zip(files, per_file):
+        assert _rows(got) == _rows(decode_ft8_from_wave(path, max_candidates=300, min_score=2)), path
+    assert sum(len(r) for r in per_file) >= 3
+    out = capsys.readouterr().out
+    assert all(f"== {p}" in out for p in files)
+
+
 def test_stft_i16_equals_f32(gpu):
     import torch
     from ft8_demodulator_amd import _device, read_wave_file
