@@ -42,10 +42,13 @@ def _worker(rank, world, port, n_slots, q):
         flat = gathered_records(s_all, stot)
         sized = (list(s_all.shape), stot.tolist(), flat["slot"].tolist(), flat["payload"][:, 0].tolist(),
                  [int(b) for b in flat.view(np.uint8).reshape(-1, 40)[:, 0]])
+        # a step that decodes nothing anywhere: a zero-row exchange, an empty gathered array
+        z_all, zc_all, ztot = gather_decodes(rec, torch.zeros_like(cnt), cap)
+        zero = (list(z_all.shape), zc_all.tolist(), ztot.tolist(), len(gathered_records(z_all, ztot)))
         q.put((rank, lo, hi, r_all.view(world, hi - lo, cap, 40)[:, :, 0, 0].tolist(), c_all.tolist(),
-               compact, dc_all.tolist(), tot.tolist(), sized))
+               compact, dc_all.tolist(), tot.tolist(), (sized, zero)))
       except Exception as e:  # noqa: BLE001
-        q.put((rank, "error", repr(e), None, None, None, None, None, None))
+        q.put((rank, "error", repr(e), None, None, None, None, None, (None, None)))
         raise
     finally:
         dist.destroy_process_group()
@@ -73,7 +76,8 @@ def test_gloo_world2_gather():
     for p in ps:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for rank, lo, hi, recs, cnts, compact, dcnts, tot, sized in out:
+    for rank, lo, hi, recs, cnts, compact, dcnts, tot, (sized, zero) in out:
+        assert zero == ([2, 0, 40], [[0, 0, 0, 0], [0, 0, 0, 0]], [0, 0], 0)
         assert recs == [[0, 1, 2, 3], [4, 5, 6, 7]]
         assert cnts == [[0, 1, 2, 3], [0, 1, 2, 3]]
         # compacted: slot s contributes min(count, cap) rows tagged s, in slot order; rank 1 holds
