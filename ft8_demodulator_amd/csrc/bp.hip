@@ -62,6 +62,9 @@ constexpr int kProdGroup = BP_PROD_GROUP;
 #ifndef BP_FIRST_SWEEP
 #define BP_FIRST_SWEEP 1  // first sweep (all tov 0): one fast_tanh per variable instead of per edge
 #endif
+#ifndef BP_SWEEP_TEST
+#define BP_SWEEP_TEST 1  // one short-division test per sweep (on the V->C arguments) instead of per group
+#endif
 [[maybe_unused]] constexpr double kClip2 = 2.0 * 4.97;  // exact: twice fast_tanh's clip bound
 #ifndef BP_GRID_CUS
 #define BP_GRID_CUS 256  // CUs the persistent grid covers (experiments only)
@@ -134,15 +137,20 @@ __device__ __forceinline__ void div_fast(double* q, const double* x, const doubl
 }
 
 template <int N, bool NEG2 = false>
-__device__ __forceinline__ void div_rn(double* q, const double* x, const double* y_in) {
+__device__ __forceinline__ void div_rn(double* q, const double* x, const double* y_in, bool fast = false) {
   // |x| < 2^900 always holds here (clamped / bounded inputs).  A NaN numerator yields NaN on either
   // path (only its payload could differ, which no later comparison or clip can observe), so the
-  // test is on the smallest |x| alone: two v_min + one compare per group, and one ballot
-  double mn = __builtin_fabs(x[0]);
+  // test is on the smallest |x| alone: two v_min + one compare per group, and one ballot -- unless
+  // the caller established the short path for the whole wave (fast)
+  bool ok = fast;
+  if (!ok) {
+    double mn = __builtin_fabs(x[0]);
 #pragma unroll
-  for (int i = 1; i < N; ++i) mn = __builtin_fmin(mn, __builtin_fabs(x[i]));
+    for (int i = 1; i < N; ++i) mn = __builtin_fmin(mn, __builtin_fabs(x[i]));
+    ok = __ballot(mn >= 0x1p-960) == __builtin_amdgcn_read_exec();
+  }
   double r[N], e[N], m[N];
-  if (__ballot(mn >= 0x1p-960) == __builtin_amdgcn_read_exec()) {
+  if (ok) {
 #pragma unroll
     for (int i = 0; i < N; ++i) r[i] = __builtin_amdgcn_rcp(y_in[i]);
 #pragma unroll
@@ -615,17 +623,23 @@ __device__ __forceinline__ double clip2(double T, bool nan_in) {
 
 // fast_tanh (ldpc_decoder.py:11-20) of kDivGroup clipped arguments in place: y = clip(T, +-2 c) in,
 // toc out (see the sweep's phase C for the scaling argument)
-__device__ __forceinline__ void tanh_group(double* v) {
+// fast: the caller established the short division for the whole wave (sweep_fast)
+__device__ __forceinline__ void tanh_group(double* v, bool fast = false) {
   double na[kDivGroup], nb[kDivGroup];
-  double mn = INFINITY;
 #pragma unroll
   for (int i = 0; i < kDivGroup; ++i) {
     const double yv = v[i], z = yv * yv;
     na[i] = yv * (15120.0 + z * (420.0 + z));
     nb[i] = -30240.0 + z * (-3360.0 + z * -30.0);
-    mn = __builtin_fmin(mn, __builtin_fabs(na[i]));
   }
-  if (__ballot(mn >= 0x1p-480) == __builtin_amdgcn_read_exec()) {
+  bool ok = fast;
+  if (!ok) {
+    double mn = INFINITY;
+#pragma unroll
+    for (int i = 0; i < kDivGroup; ++i) mn = __builtin_fmin(mn, __builtin_fabs(na[i]));
+    ok = __ballot(mn >= 0x1p-480) == __builtin_amdgcn_read_exec();
+  }
+  if (ok) {
     div_fast<kDivGroup>(v, na, nb);
   } else {
 #pragma unroll
@@ -638,8 +652,44 @@ __device__ __forceinline__ void tanh_group(double* v) {
   }
 }
 
+// min(|hi dword|) of three doubles, the hi dwords read as float32 (v_min3_f32 with abs modifiers).
+// For a finite double, |x| >= 2^k (k integer) iff the float32 view of its hi dword, sign cleared,
+// is >= the view of 2^k's hi dword (the low dword of 2^k is 0, and non-negative float32 bit
+// patterns order as integers).  A NaN's hi dword reads as a quiet float32 NaN, which v_min3 skips.
+__device__ __forceinline__ float min3_abs_hi(double a, double b, double c) {
+  float m;
+  asm("v_min3_f32 %0, |%1|, |%2|, |%3|"
+      : "=v"(m)
+      : "v"(__double2hiint(a)), "v"(__double2hiint(b)), "v"(__double2hiint(c)));
+  return m;
+}
+
+// Per-sweep short-division test (BP_SWEEP_TEST): true when every V->C argument y of the wave
+// (3 x 3 per lane, after np.clip) has |y| >= 2^-100 -- or is NaN, which either division path
+// turns into the same NaN (see div_rn).  That one test admits both phases' short divisions:
+//   * fast_tanh: |A| = |y| (15120 + z (420 + z)) >= 2^-100 * 15120 > 2^-480 (tanh_group's test);
+//   * fast_atanh: every toc stored this sweep is RN(A/B) with |A/B| >= |y| / 10 (the ratio
+//     (15120 + 420 z + z^2) / (30240 + 3360 z + 30 z^2) is >= 0.1013 for z = y^2 <= 98.8), so
+//     |toc| >= 2^-104, and |toc| <= 1.0073; a product of six of them (or of five and the 1.0
+//     that pads a degree-6 row) stays >= 2^-625 with no subnormal step, and the numerator
+//     x (945 + x^2 (-735 + 64 x^2)) has |.| >= 219 |x| > 2^-960 (div_rn's test); the
+//     denominators are the same normal values on either path.
+// 4 v_min3_f32 + 1 compare per sweep instead of 3-4 VALU per division group (6 groups per sweep).
+__device__ __forceinline__ bool sweep_fast(const double (&y)[kVarSlots][3]) {
+  static_assert(kVarSlots == 3, "three variable slots");
+  const float m0 = min3_abs_hi(y[0][0], y[0][1], y[0][2]);
+  const float m1 = min3_abs_hi(y[1][0], y[1][1], y[1][2]);
+  const float m2 = min3_abs_hi(y[2][0], y[2][1], y[2][2]);
+  float m;
+  asm("v_min3_f32 %0, %1, %2, %3" : "=v"(m) : "v"(m0), "v"(m1), "v"(m2));
+  // hi dword of 2^-100: biased exponent 923 << 20
+  const float thr = __int_as_float(923 << 20);
+  return __ballot(m < thr) == 0;
+}
+
 // tov = -2 fast_atanh(Tmn) (ldpc_decoder.py:22-30, 108) of kDivGroup products in place.
-__device__ __forceinline__ void atanh_group(double* v) {
+// fast: the caller established the short division for the whole wave (sweep_fast).
+__device__ __forceinline__ void atanh_group(double* v, bool fast = false) {
   double na[kDivGroup], nb[kDivGroup];
 #pragma unroll
   for (int i = 0; i < kDivGroup; ++i) {
@@ -649,7 +699,7 @@ __device__ __forceinline__ void atanh_group(double* v) {
     // exact (terms too small to scale exactly are absorbed by the constant they meet)
     nb[i] = (-472.5 + x2 * (525.0 + x2 * -112.5));
   }
-  div_rn<kDivGroup, true>(v, na, nb);
+  div_rn<kDivGroup, true>(v, na, nb, fast);
 }
 
 // Phase D's products: for each of the lane's edge slots, the product of the other toc of the edge's
@@ -838,15 +888,16 @@ __global__ __launch_bounds__(kWave, BP_LB_WAVES) void k_bp(BpArgs a) {
       // runs the reference form on x = -y / 2 (tanh_group).
       // variable-major, straight from phase A's registers into each edge's slot
       static_assert(kDivGroup == 3 && kVarSlots == 3, "a division group is one variable's edges");
+      const bool fast = BP_SWEEP_TEST && sweep_fast(y);
       if (sweep0) {  // one fast_tanh per variable
         double v[kVarSlots] = {y[0][0], y[1][0], y[2][0]};
-        tanh_group(v);
+        tanh_group(v, fast);
 #pragma unroll
         for (int j = 0; j < kVarSlots; ++j) y[j][0] = y[j][1] = y[j][2] = v[j];
       }
 #pragma unroll
       for (int j = 0; j < kVarSlots; ++j) {
-        if (!sweep0) tanh_group(y[j]);
+        if (!sweep0) tanh_group(y[j], fast);
         if (j < kVarSlots - 1 || var2) {
           *(__attribute__((address_space(3))) double*)(uintptr_t)tb.va[j] = y[j][0];
           *(__attribute__((address_space(3))) double*)(uintptr_t)tb.va1[j] = y[j][1];
@@ -859,7 +910,7 @@ __global__ __launch_bounds__(kWave, BP_LB_WAVES) void k_bp(BpArgs a) {
       // (D) check -> variable messages: tov = -2 fast_atanh(product of the other toc of the check)
       check_products(x, la, lane);
 #pragma unroll
-      for (int g = 0; g < kEdgeSlots; g += kDivGroup) atanh_group(&x[g]);
+      for (int g = 0; g < kEdgeSlots; g += kDivGroup) atanh_group(&x[g], fast);
 #pragma unroll
       for (int i = 0; i < kEdgeSlots; ++i)
         if (i < kEdgeSlots - 1 || lane + kWave * i < FT8_LDPC_E)
