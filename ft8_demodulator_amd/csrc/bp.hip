@@ -137,17 +137,17 @@ __device__ __forceinline__ void div_fast(double* q, const double* x, const doubl
 }
 
 template <int N, bool NEG2 = false>
-__device__ __forceinline__ void div_rn(double* q, const double* x, const double* y_in, bool fast = false) {
+__device__ __forceinline__ void div_rn(double* q, const double* x, const double* y_in, int fast = 0) {
   // |x| < 2^900 always holds here (clamped / bounded inputs).  A NaN numerator yields NaN on either
   // path (only its payload could differ, which no later comparison or clip can observe), so the
   // test is on the smallest |x| alone: two v_min + one compare per group, and one ballot -- unless
   // the caller established the short path for the whole wave (fast)
-  bool ok = fast;
+  int ok = fast;
   if (!ok) {
     double mn = __builtin_fabs(x[0]);
 #pragma unroll
     for (int i = 1; i < N; ++i) mn = __builtin_fmin(mn, __builtin_fabs(x[i]));
-    ok = __ballot(mn >= 0x1p-960) == __builtin_amdgcn_read_exec();
+    ok = __ballot(mn >= 0x1p-960) == __builtin_amdgcn_read_exec() ? 1 : 0;
   }
   double r[N], e[N], m[N];
   if (ok) {
@@ -624,7 +624,7 @@ __device__ __forceinline__ double clip2(double T, bool nan_in) {
 // fast_tanh (ldpc_decoder.py:11-20) of kDivGroup clipped arguments in place: y = clip(T, +-2 c) in,
 // toc out (see the sweep's phase C for the scaling argument)
 // fast: the caller established the short division for the whole wave (sweep_fast)
-__device__ __forceinline__ void tanh_group(double* v, bool fast = false) {
+__device__ __forceinline__ void tanh_group(double* v, int fast = 0) {
   double na[kDivGroup], nb[kDivGroup];
 #pragma unroll
   for (int i = 0; i < kDivGroup; ++i) {
@@ -632,12 +632,12 @@ __device__ __forceinline__ void tanh_group(double* v, bool fast = false) {
     na[i] = yv * (15120.0 + z * (420.0 + z));
     nb[i] = -30240.0 + z * (-3360.0 + z * -30.0);
   }
-  bool ok = fast;
+  int ok = fast;  // an int, not a bool: a bool crossing blocks would be kept as a VALU lane mask
   if (!ok) {
     double mn = INFINITY;
 #pragma unroll
     for (int i = 0; i < kDivGroup; ++i) mn = __builtin_fmin(mn, __builtin_fabs(na[i]));
-    ok = __ballot(mn >= 0x1p-480) == __builtin_amdgcn_read_exec();
+    ok = __ballot(mn >= 0x1p-480) == __builtin_amdgcn_read_exec() ? 1 : 0;
   }
   if (ok) {
     div_fast<kDivGroup>(v, na, nb);
@@ -689,7 +689,7 @@ __device__ __forceinline__ bool sweep_fast(const double (&y)[kVarSlots][3]) {
 
 // tov = -2 fast_atanh(Tmn) (ldpc_decoder.py:22-30, 108) of kDivGroup products in place.
 // fast: the caller established the short division for the whole wave (sweep_fast).
-__device__ __forceinline__ void atanh_group(double* v, bool fast = false) {
+__device__ __forceinline__ void atanh_group(double* v, int fast = 0) {
   double na[kDivGroup], nb[kDivGroup];
 #pragma unroll
   for (int i = 0; i < kDivGroup; ++i) {
@@ -776,7 +776,10 @@ __global__ __launch_bounds__(kWave, BP_LB_WAVES) void k_bp(BpArgs a) {
 #pragma unroll
     for (int j = 0; j < kVarSlots; ++j) {
       const int n = lane + kWave * j;
-      cv_[j] = n < FT8_LDPC_N ? a.llr_in[(int64_t)item * FT8_LDPC_N + n] : 0.0;
+      // padding variables (slot 2, lanes >= 46): codeword -1.0, and their three tov read the
+      // constant 1.0, so every V->C argument is (-1 + 1) + 1 = 1.0 after the first sweep (-1.0 in
+      // it): harmless, never tiny (the wave stays on the short division), never stored
+      cv_[j] = n < FT8_LDPC_N ? a.llr_in[(int64_t)item * FT8_LDPC_N + n] : -1.0;
     }
 
     // NaN LLRs must survive np.clip as NaN; the clip's v_min/v_max would turn them into the bound,
@@ -852,9 +855,6 @@ __global__ __launch_bounds__(kWave, BP_LB_WAVES) void k_bp(BpArgs a) {
             for (int e = 0; e < 3; ++e) y[j][e] = clip2(y[j][e], false);
         }
       }
-      // padding variables (slot 2, lanes >= 46) evaluate a harmless 1.0 so that their wave stays on
-      // the short division, and store nothing
-      if (!var2) y[kVarSlots - 1][0] = y[kVarSlots - 1][1] = y[kVarSlots - 1][2] = 1.0;
       hd[kVarSlots - 1] &= var2_mask;
       // all-zero hard decision -> stop (ldpc_decoder.py:76-78)
       if ((hd[0] | hd[1] | hd[2]) == 0) break;
@@ -888,7 +888,9 @@ __global__ __launch_bounds__(kWave, BP_LB_WAVES) void k_bp(BpArgs a) {
       // runs the reference form on x = -y / 2 (tanh_group).
       // variable-major, straight from phase A's registers into each edge's slot
       static_assert(kDivGroup == 3 && kVarSlots == 3, "a division group is one variable's edges");
-      const bool fast = BP_SWEEP_TEST && sweep_fast(y);
+      // wave-uniform int (a bool crossing blocks would be kept as a VALU lane mask)
+      int fast = __builtin_amdgcn_readfirstlane(BP_SWEEP_TEST && sweep_fast(y) ? 1 : 0);
+      asm volatile("" : "+s"(fast));  // opaque SGPR: branches test it with s_cmp
       if (sweep0) {  // one fast_tanh per variable
         double v[kVarSlots] = {y[0][0], y[1][0], y[2][0]};
         tanh_group(v, fast);
