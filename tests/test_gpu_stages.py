@@ -198,6 +198,15 @@ def test_bp_extreme_inputs_vs_oracle(gpu, oracle):
     v = rng.standard_normal(174)
     v[:60] = 0.0
     vecs.append(v)
+    # around k_bp's per-sweep short-division bound (|V->C argument| >= 2^-100, bp.hip sweep_fast):
+    # whole vectors just above / below it, and normal vectors with one or a few arguments near it
+    for scale in (2.0 ** -99, 2.0 ** -100, 2.0 ** -101, 1e-30, 1e-31):
+        vecs.append(rng.standard_normal(174) * scale)
+    for pos in ([0], [173], [5, 60, 120]):
+        for tiny in (2.0 ** -100, 2.0 ** -100 * (1 - 2.0 ** -52), 2.0 ** -101, 5e-324):
+            v = rng.standard_normal(174) * 3.0
+            v[pos] = tiny * np.sign(rng.standard_normal(len(pos)))
+            vecs.append(v)
     # NaN and infinite LLRs (bp_decode accepts any vector): np.clip keeps NaN, so it spreads
     for pos in ([3], [3, 50, 100, 171], list(range(0, 174, 5))):
         v = rng.standard_normal(174) * 2.0
