@@ -615,6 +615,20 @@ def main():
         with open(tfiles[-1]) as f:
             traffic = json.load(f).get("kernels", {})
 
+    # k_bp issue counters from the newest committed SQ pass (tools/gpu_pmc_r2.sh + tools/pmc_sq_json.py)
+    issue = None
+    qfiles = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_v*_pmc.json")), key=_rv)
+    if qfiles:
+        with open(qfiles[-1]) as f:
+            q = json.load(f).get("kernels", {}).get("k_bp<false>")
+        if q and cn["passes"]:
+            issue = {"valu_busy_per_simd": q.get("valu_busy_per_simd"),
+                     "valu_instructions_per_sweep": q["SQ_INSTS_VALU"] / (cn["passes"] / R),
+                     "source": os.path.relpath(qfiles[-1], ROOT),
+                     "note": "the exact (uncontracted, correctly rounded) FP64 instruction stream carries "
+                             "~245 algorithmic flops per lane per sweep; frac at 100% VALU busy would be "
+                             "~frac / valu_busy (DESIGN.md section 3)"}
+
     def hbm(kernel_prefix):
         for k, v in traffic.items():
             if k.startswith(kernel_prefix):
@@ -650,7 +664,8 @@ def main():
                      "frac": ach_tf / FP64_VECTOR_PEAK_TFLOPS, "traffic": hbm("ft8::k_bp"), "traffic_source": tsrc,
                      "flops_per_launch": flops, "launch_ms": bp_ms,
                      "launch_ms_from": f"HIP events around k_bp alone in {R} full steps after the timed loop",
-                     "bp_passes_per_launch": cn["passes"] / R, "candidates_per_launch": cn["candidates"] / R},
+                     "bp_passes_per_launch": cn["passes"] / R, "candidates_per_launch": cn["candidates"] / R,
+                     "issue": issue},
         "step_hbm": {"what": "BASELINE.md whole-step accounting: slots/s per GPU x B_slot algorithmic bytes "
                              "(the step is FP64-VALU bound in k_bp, so this fraction is low by construction)",
                      "bytes_per_slot": b_slot, "achieved": step_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
