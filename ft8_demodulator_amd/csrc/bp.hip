@@ -760,7 +760,13 @@ __global__ __launch_bounds__(kWave, BP_LB_WAVES) void k_bp(BpArgs a) {
     if (lane == 0) item = atomicAdd(a.work, 1u);
     // wave-uniform: candidate metadata then lives in SGPRs (scalar loads), not VGPRs
     item = __builtin_amdgcn_readfirstlane(__shfl(item, 0));
-    if ((int)item >= a.n_items) break;
+    if ((int)item >= a.n_items) {
+      // every wave's claims end with exactly one ticket >= n_items, so the wave holding the last
+      // ticket (n_items + waves - 1) claims after everyone else: it leaves the counter at 0 for the
+      // next launch (no memset kernel per launch; a fresh counter buffer is zeroed once, capi.hip)
+      if (lane == 0 && item == (unsigned)a.n_items + gridDim.x - 1u) atomicExch(a.work, 0u);
+      break;
+    }
 
     int slot = 0, at = 0, af = 0, cidx = 0;
     double score = 0.0;
@@ -1092,8 +1098,7 @@ hipError_t launch_llr(const BpLaunch& L, hipStream_t s) {
 hipError_t launch_bp(const BpLaunch& L, hipStream_t s) {
   if (L.n_items <= 0) return hipSuccess;
   BpArgs a = make_args(L);
-  hipError_t e = hipMemsetAsync(L.work, 0, sizeof(unsigned), s);
-  if (e != hipSuccess) return e;
+  // L.work is 0 here: zeroed when its buffer was allocated, and every k_bp launch leaves it at 0
   const int per_simd = max(1, min(L.grid_waves, BP_WAVES_PER_EU));
   const int waves = min(L.n_items, BP_GRID_CUS * 4 * per_simd);  // resident waves, persistent
   if (L.mode == 0) hipLaunchKernelGGL(k_bp<false>, dim3(waves), dim3(kWave), 0, s, a);

@@ -109,6 +109,19 @@ struct DeviceGuard {
   }
 };
 
+int ensure(ft8_ctx* c, DevBuf& b, size_t bytes);
+
+// ensure() for a buffer that must read as zeros when (re)allocated: the k_bp work counters, which
+// every k_bp launch leaves at 0 again (bp.hip), so they are cleared only here
+int ensure_zeroed(ft8_ctx* c, DevBuf& b, size_t bytes, hipStream_t s) {
+  void* old = b.p;
+  const size_t old_cap = b.cap;
+  int rc = ensure(c, b, bytes);
+  if (rc || (b.p == old && b.cap == old_cap)) return rc;
+  hipError_t e = hipMemsetAsync(b.p, 0, b.cap, s);
+  return e == hipSuccess ? FT8_OK : hipfail(c, e, "memset");
+}
+
 int ensure(ft8_ctx* c, DevBuf& b, size_t bytes) {
   if (bytes == 0) bytes = 16;
   if (b.cap >= bytes) return FT8_OK;
@@ -507,7 +520,7 @@ int decode_pass(ft8_ctx* c, const void* d_samples, int dtype, int64_t n_samples,
   const int csz = (c->n_streams > 0 && c->chunk_slots > 0) ? c->chunk_slots : n_slots;
   const int n_chunks = (n_slots + csz - 1) / csz;
   const int n_str = (c->n_streams > 0 && n_chunks > 1) ? std::min(c->n_streams, n_chunks) : 0;
-  if ((rc = ensure(c, c->work, sizeof(unsigned) * (size_t)std::max(n_chunks, 4)))) return rc;
+  if ((rc = ensure_zeroed(c, c->work, sizeof(unsigned) * (size_t)std::max(n_chunks, 4), s))) return rc;
   hipError_t e = hipSuccess;
   if (n_str > 0) {
     while ((int)c->streams.size() < n_str) {
@@ -952,7 +965,7 @@ int ft8_bp(ft8_ctx* c, const double* d_llr, int32_t n, int32_t max_iterations, u
   if (n <= 0) return FT8_OK;
   DeviceGuard dg(c->device);
   int rc;
-  if ((rc = ensure(c, c->work, 16))) return rc;
+  if ((rc = ensure_zeroed(c, c->work, 16, (hipStream_t)stream))) return rc;
   BpLaunch L{};
   L.mode = 2;
   L.llr_in = d_llr;
