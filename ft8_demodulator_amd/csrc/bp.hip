@@ -926,10 +926,15 @@ __global__ __launch_bounds__(kWave, BP_LB_WAVES) void k_bp(BpArgs a) {
       passes++;
       sweep_sync();
     }
-    // the hard decision of the last evaluated sweep (all zero if no sweep ran)
+    // the hard decision of the last evaluated sweep (all zero if no sweep ran), staged only when
+    // something reads it: the plain output, or the payload of a candidate that converged
+    // (min_errors is wave-uniform; most candidates never converge and skip the packing)
+    const bool pack = a.res && min_errors == 0;
+    if (a.plain_out || pack) {
 #pragma unroll
-    for (int j = 0; j < kVarSlots; ++j) L.bits[lane + kWave * j] = (uint8_t)((hd[j] >> lane) & 1u);
-    __syncthreads();
+      for (int j = 0; j < kVarSlots; ++j) L.bits[lane + kWave * j] = (uint8_t)((hd[j] >> lane) & 1u);
+      __syncthreads();
+    }
     st_cand++;
     st_iter += entered;
     st_pass += passes;
@@ -941,7 +946,7 @@ __global__ __launch_bounds__(kWave, BP_LB_WAVES) void k_bp(BpArgs a) {
       for (int n = lane; n < FT8_LDPC_N; n += kWave) a.plain_out[(int64_t)item * FT8_LDPC_N + n] = L.bits[n];
     if (a.res) {
       // pack 91 bits MSB first (ft8_decode.py:200-215)
-      if (lane < 12) {  // lane l packs decision bytes 8l..8l+7 (one 8-byte LDS read)
+      if (pack && lane < 12) {  // lane l packs decision bytes 8l..8l+7 (one 8-byte LDS read)
         const uint64_t w = *reinterpret_cast<const uint64_t*>(&L.bits[8 * lane]);
         const uint32_t lo = (uint32_t)w, hi = (uint32_t)(w >> 32);
         unsigned byte = 0;
