@@ -4,9 +4,10 @@ One step = one ft8_decode_batch over a batch of 256 independent synthetic 15-s s
 (50 GFSK signals per slot at SNR U(-24, -10) dB, full-band convention; K=300, min_score=2,
 20 BP iterations): STFT -> Costas sync -> selection -> LLR -> BP -> CRC, samples already
 resident in HBM.  With N > 1 GPUs each rank decodes its own 256 slots (weak scaling) and the
-step ends with an RCCL all-gather of every rank's result records (the path's one exchange).
+step ends with an RCCL all-gather of every rank's decodes, packed on the device (the path's one
+exchange; no host sync inside the step).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--slots S] [--no-cpu]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--slots S] [--no-cpu] [--gather]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
 `python bench.py --gpus N` with N > 1 and no WORLD_SIZE in the environment launches the N ranks
@@ -29,6 +30,9 @@ Prints ONE JSON line on rank 0.  Besides the contract fields it carries:
   cpu_baseline  the oracle port (oracle/, C + scipy) on the first slots of rank 0's own batch -- the
                 same bytes the GPU decodes (rank 0, N=1)
   parity        those slots' GPU decodes vs the oracle's: payload + CRC multisets, ordered lists
+  gather        (N > 1 or --gather) the last timed step's decode exchange: backend, rows and bytes per rank
+  gather_n1     (N = 1) steps with vs without the N > 1 exchange (device pack + RCCL all-gather over a
+                world-size-1 group), interleaved blocks: its cost per step
   reference_measured  the reference's own single-thread figure, for context
 """
 import argparse
@@ -401,6 +405,78 @@ REFERENCE_MEASURED = {
 STAGE_ORDER = ("stft", "score", "select", "llr", "bp", "compact")
 
 
+def counters_for_build(pattern, build_id):
+    """The newest committed profiles/<pattern> summary whose build_id equals the running library's
+    -> (kernels dict, relative path); (None, "stale: <newest file> (build <id>)") when none matches,
+    (None, None) when there is none."""
+    import glob
+
+    def _rv(p_):  # rNN[_vK]_... -> (NN, K)
+        parts = os.path.basename(p_)[1:].split("_")
+        return int(parts[0]), int(parts[1][1:]) if parts[1].startswith("v") and parts[1][1:].isdigit() else -1
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)), key=_rv)
+    for f in reversed(files):
+        with open(f) as fh:
+            d = json.load(fh)
+        if d.get("build_id") == build_id:
+            return d.get("kernels", {}), os.path.relpath(f, ROOT)
+    if files:
+        with open(files[-1]) as fh:
+            old = json.load(fh).get("build_id")
+        return None, f"stale: {os.path.relpath(files[-1], ROOT)} (build {old}); no summary of this build"
+    return None, None
+
+
+def rccl_world1(dev):
+    """A world-size-1 RCCL ("nccl") process group on `dev` (127.0.0.1 rendezvous)."""
+    import socket
+    import torch.distributed as dist
+    if dist.is_initialized():
+        return
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1, device_id=dev)
+
+
+def gather_leg(dec, x, dev, S, steps, rounds=3):
+    """N = 1: the cost of the N > 1 step's exchange, on this GPU -- blocks of `steps` plain steps and
+    of `steps` steps that also pack the decodes (ft8_pack_decodes) and all-gather them over a
+    world-size-1 RCCL group, interleaved `rounds` times; ms per step of each (best block)."""
+    import torch
+    import torch.distributed as dist
+    from ft8_demodulator_amd.distributed import DecodeGatherer
+    rccl_world1(dev)
+    g = DecodeGatherer(S, dec.cap)
+    last = []
+
+    def block(with_gather):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            out, counts = dec.run(x)
+            if with_gather:
+                last[:] = [g.start(out, counts)]
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / steps * 1e3
+
+    block(True)
+    plain, gath = [], []
+    for _ in range(rounds):
+        plain.append(block(False))
+        gath.append(block(True))
+    recs, _, tot = last[0].resolve()
+    ok = recs.shape[1] == int(tot[0])
+    dist.destroy_process_group()
+    return {"backend": "nccl (RCCL), world size 1", "steps_per_block": steps, "rounds": rounds,
+            "ms_per_step_plain": min(plain), "ms_per_step_with_gather": min(gath),
+            "overhead_pct": (min(gath) / min(plain) - 1.0) * 100.0,
+            "blocks_plain_ms": plain, "blocks_gather_ms": gath,
+            "rows_per_rank_sent": g.capacity, "decodes_gathered_last_step": int(tot[0]), "resolved_ok": bool(ok),
+            "what": "each gather step: ft8_pack_decodes (one HIP kernel) + dist.all_gather_into_tensor of the "
+                    "packed buffer on the decode stream, no host sync; the last step's exchange resolved after"}
+
+
 def launch_ranks(args):
     """--gpus N > 1 without a launcher: start N ranks under torch.distributed.run as a child
     process (this process never touches the GPU) and return its exit code."""
@@ -436,6 +512,11 @@ def main():
     ap.add_argument("--no-h2d", action="store_true", help="skip the PCIe-inclusive streaming leg")
     ap.add_argument("--no-subtract", action="store_true", help="skip the config-4 subtract-and-redecode leg")
     ap.add_argument("--no-drift", action="store_true", help="skip the frequency-drift correction leg")
+    ap.add_argument("--gather", action="store_true",
+                    help="N = 1: every timed step also packs its decodes and all-gathers them over a world-size-1 "
+                         "RCCL group (the per-step exchange of the N > 1 path)")
+    ap.add_argument("--no-gather-leg", action="store_true",
+                    help="skip the N = 1 leg that times steps with and without the RCCL exchange")
     ap.add_argument("--share-gpu", action="store_true",
                     help="rehearsal of the N > 1 path on a one-GPU box: every rank on cuda:0, gloo instead of "
                          "RCCL (exercises the launch, sharding and decode gather; not a measurement)")
@@ -477,9 +558,11 @@ def main():
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=dev)
+    elif args.gather:
+        rccl_world1(dev)
 
     from ft8_demodulator_amd import SlotDecoder, synth, _lib
-    from ft8_demodulator_amd.distributed import gather_decodes
+    from ft8_demodulator_amd.distributed import DecodeGatherer
 
     # the batch: slots synthesised on the CPU for the CPU leg are uploaded as-is (same bytes), the
     # rest synthesised on the GPU with the same per-slot seeds
@@ -499,14 +582,17 @@ def main():
     ctx.set_timing(True)   # allocates the device BP work counters; no events in the timed loop
     ctx.set_timing(False)
 
-    # N > 1: every step ends with the data-sized all-gather of the decodes (totals, then exactly
-    # max(total) rows per rank), records carrying global slot ids
-    gathered = []
+    # N > 1 (or --gather): every step ends with the decode exchange -- ft8_pack_decodes on the device,
+    # one all-gather of the packed buffer, no host sync (distributed.DecodeGatherer); the last
+    # step's exchange is resolved after the timed loop.  Records carry global slot ids.
+    exchange = world > 1 or args.gather
+    gatherer = DecodeGatherer(S, dec.cap, slot_offset=rank * S) if exchange else None
+    handles = []
 
     def step():
         out, counts = dec.run(x)
-        if world > 1:
-            gathered[:] = [gather_decodes(out, counts, dec.cap, slot_offset=rank * S)]
+        if exchange:
+            handles[:] = [gatherer.start(out, counts)]
         return counts
 
     for _ in range(args.warmup):
@@ -523,6 +609,13 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     decoded = int(counts.sum().item())
+    gather = None
+    if exchange:
+        recs_g, _, totals_g = handles[0].resolve()   # collective: every rank resolves the last step's
+        gather = {"backend": dist.get_backend(), "world": world,
+                  "rows_per_rank_sent": gatherer.capacity, "bytes_per_rank_sent": 8 + 4 * S + gatherer.capacity * 40,
+                  "decodes_per_rank_last_step": totals_g.cpu().tolist(), "overflow_exchanges": gatherer.grown,
+                  "host_sync_per_step": False}
 
     # per-kernel durations inside the real step sequence: one pass of `stage_steps` steps per stage,
     # with HIP events bracketing only that stage's kernel (the rest of the step runs undisturbed);
@@ -602,32 +695,27 @@ def main():
     if world == 1 and not args.no_subtract:
         sub = subtract_redecode(dev)
 
-    # HBM bytes per launch from the committed rocprofv3 PMC summary (tools/pmc_traffic.py; FETCH_SIZE
-    # and WRITE_SIZE passes of the same 256-slot workload), or null when it is absent
-    import glob
-    traffic, tsrc = {}, None
-    def _rv(p_):  # rNN[_vK]_pmc_traffic.json -> (NN, K)
-        parts = os.path.basename(p_)[1:].split("_")
-        return int(parts[0]), int(parts[1][1:]) if parts[1].startswith("v") and parts[1][1:].isdigit() else -1
-    tfiles = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")), key=_rv)
-    if tfiles:
-        tsrc = os.path.relpath(tfiles[-1], ROOT)
-        with open(tfiles[-1]) as f:
-            traffic = json.load(f).get("kernels", {})
-
-    # k_bp issue counters from the newest committed SQ pass (tools/gpu_pmc_r2.sh + tools/pmc_sq_json.py)
+    # HBM bytes and issue counters per launch from the committed rocprofv3 PMC summaries
+    # (tools/pmc_traffic.py: FETCH_SIZE / WRITE_SIZE passes; tools/pmc_sq_json.py: the SQ pass), each
+    # stamped with the build_id it measured: only a summary of THIS build is reported, else null
+    gather_n1 = None
+    if world == 1 and not args.gather and not args.no_gather_leg:
+        gather_n1 = gather_leg(dec, x, dev, S, args.steps)
+    build_id = _lib.lib().ft8_build_id().decode()
+    traffic, tsrc = counters_for_build("r*_pmc_traffic.json", build_id)
+    qdata, qsrc = counters_for_build("r*_v*_pmc.json", build_id)
     issue = None
-    qfiles = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_v*_pmc.json")), key=_rv)
-    if qfiles:
-        with open(qfiles[-1]) as f:
-            q = json.load(f).get("kernels", {}).get("k_bp<false>")
-        if q and cn["passes"]:
-            issue = {"valu_busy_per_simd": q.get("valu_busy_per_simd"),
-                     "valu_instructions_per_sweep": q["SQ_INSTS_VALU"] / (cn["passes"] / R),
-                     "source": os.path.relpath(qfiles[-1], ROOT),
-                     "note": "the exact (uncontracted, correctly rounded) FP64 instruction stream carries "
-                             "~245 algorithmic flops per lane per sweep; frac at 100% VALU busy would be "
-                             "~frac / valu_busy (DESIGN.md section 3)"}
+    q = (qdata or {}).get("k_bp<false>")
+    if q and cn["passes"]:
+        issue = {"valu_busy_per_simd": q.get("valu_busy_per_simd"),
+                 "valu_instructions_per_sweep": q["SQ_INSTS_VALU"] / (cn["passes"] / R),
+                 "source": qsrc,
+                 "note": "the exact (uncontracted, correctly rounded) FP64 instruction stream carries "
+                         "~245 algorithmic flops per lane per sweep; frac at 100% VALU busy would be "
+                         "~frac / valu_busy (DESIGN.md section 3)"}
+    elif qsrc:
+        issue = {"source": qsrc}
+    traffic = traffic or {}
 
     def hbm(kernel_prefix):
         for k, v in traffic.items():
@@ -655,8 +743,10 @@ def main():
                    "slots_per_gpu": S, "sample_rate": 12000, "samples_per_slot": int(x.shape[1]),
                    "max_candidates": 300, "min_score": 2, "max_iterations": 20,
                    "parallelism": f"slot-sharded x{world}" + (
-                       ", one data-sized RCCL all-gather of the device-compacted decodes per step"
-                       if world > 1 else "")},
+                       (", one all-gather per step of the device-packed decodes over "
+                        + ("gloo (--share-gpu rehearsal, every rank on cuda:0)" if args.share_gpu else "RCCL")
+                        + (" (world size 1, --gather)" if world == 1 else ""))
+                       if exchange else "")},
         "ldpc_candidates_per_s": cand_per_s,
         "decodes_per_step": decoded,  # successful decodes in one step's batch (every step decodes the same batch)
         "roofline": {"kernel": "k_bp (float64 BP + CRC)", "bound": "fp64-valu",
@@ -686,15 +776,15 @@ def main():
         "cpu_baseline": cpu,
         "parity": parity,
         "reference_measured": REFERENCE_MEASURED,
-        "build_id": _lib.lib().ft8_build_id().decode(),
+        "build_id": build_id,
     }
-    if world > 1:
-        recs, _, totals = gathered[0]
-        line["gather"] = {"rows_per_rank": int(recs.shape[1]), "bytes_per_rank": int(recs.shape[1]) * 40 + 4 * S + 8,
-                          "decodes_per_rank_last_step": totals.cpu().tolist(), "sized_from_data": True}
+    if gather is not None:
+        line["gather"] = gather
+    if gather_n1 is not None:
+        line["gather_n1"] = gather_n1
     if rank == 0:
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

@@ -126,6 +126,8 @@ def lib():
             "ft8_replay_stage": ([vp, i32, i32, vp], ctypes.c_int),
             "ft8_set_timing_stages": ([vp, ctypes.c_uint32], ctypes.c_int),
             "ft8_sync_score": ([vp, vp, ctypes.c_int, i32, i32, i32, i32, vp, i32, vp, vp, vp], ctypes.c_int),
+            "ft8_pack_bytes": ([i32, i32], i64),
+            "ft8_pack_decodes": ([vp, vp, vp, i32, i32, i32, i32, vp, vp, vp], ctypes.c_int),
         }
         for name, (args, res) in sig.items():
             fn = getattr(L, name)
@@ -168,7 +170,8 @@ EXPORTED_SYMBOLS = (
     "ft8_stft", "ft8_sync_select", "ft8_llr", "ft8_normalize", "ft8_bp", "ft8_decode_batch", "ft8_select_warnings",
     "ft8_crc14", "ft8_ldpc_check", "ft8_set_timing", "ft8_get_timing", "ft8_get_counters", "ft8_set_pipeline",
     "ft8_encode", "ft8_synthesize", "ft8_subtract", "ft8_stft_argmax", "ft8_drift_fit", "ft8_drift_correct",
-    "ft8_build_id", "ft8_build_flags", "ft8_replay_stage", "ft8_set_timing_stages", "ft8_sync_score")
+    "ft8_build_id", "ft8_build_flags", "ft8_replay_stage", "ft8_set_timing_stages", "ft8_sync_score",
+    "ft8_pack_bytes", "ft8_pack_decodes")
 
 
 def limits():

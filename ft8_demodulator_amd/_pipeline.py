@@ -178,6 +178,17 @@ def records_to_results(recs: np.ndarray, sample_rate: int, bins_per_tone: int, w
     return out
 
 
+def warn_truncated(counts: np.ndarray, cap: int, stacklevel: int = 2) -> None:
+    """RuntimeWarning when a slot decoded more messages than its record capacity holds (the device
+    keeps the first `cap` in candidate order and counts the rest)."""
+    over = np.nonzero(counts > cap)[0]
+    if over.size:
+        import warnings
+        warnings.warn(f"{over.size} slot(s) decoded more messages than max_results_per_slot={cap} "
+                      f"(e.g. slot {int(over[0])}: {int(counts[over[0]])}); the records beyond it were dropped",
+                      RuntimeWarning, stacklevel=stacklevel + 1)
+
+
 class SlotDecoder:
     """Batched decode of independent slots on one GPU: [B, N] samples -> per-slot decodes.
 
@@ -253,12 +264,7 @@ class SlotDecoder:
         n_slots = len(c)
         recs = out[: n_slots * self.cap * _lib.RESULT_DTYPE.itemsize].cpu().numpy().view(_lib.RESULT_DTYPE)
         recs = recs.reshape(n_slots, self.cap) if n_slots else recs.reshape(0, self.cap)
-        over = np.nonzero(c > self.cap)[0]
-        if over.size:
-            import warnings
-            warnings.warn(f"{over.size} slot(s) decoded more messages than max_results_per_slot={self.cap} "
-                          f"(e.g. slot {int(over[0])}: {int(c[over[0]])}); the records beyond it were dropped",
-                          RuntimeWarning, stacklevel=2)
+        warn_truncated(c, self.cap, stacklevel=3)
         return [recs[s, : min(int(c[s]), self.cap)].copy() for s in range(n_slots)]
 
     def decode(self, samples, int16_is_pcm=True):

@@ -39,36 +39,24 @@ constexpr int kChkSlots = (FT8_LDPC_M + kWave - 1) / kWave;   // 2
 // dummy edges/bits/checks that read and write only padding slots of the LDS arrays, so the three
 // phases are branch-free and the per-lane chains (18 IEEE divisions per sweep) interleave.
 
-#ifndef BP_DIV_GROUP
-#define BP_DIV_GROUP 3
-#endif
-constexpr int kDivGroup = BP_DIV_GROUP;  // divisions interleaved at a time (kEdgeSlots % kDivGroup == 0)
-#ifndef BP_PROD_GROUP
-#define BP_PROD_GROUP 3
-#endif
-constexpr int kProdGroup = BP_PROD_GROUP;
-#ifndef BP_WAVES_PER_EU
-#define BP_WAVES_PER_EU 4
-#endif
-// The register budget the compiler is given: at a 4-wave budget (128 VGPRs) the allocator spills
-// ~50 VGPRs of the fused sweep to scratch, although under a 3-wave budget it needs only 118 -- which
-// still leaves 4 waves resident per SIMD (512 / 120), the residency the grid is sized for.
-#ifndef BP_LB_WAVES
-#define BP_LB_WAVES 3
-#endif
-#ifndef BP_SKIP_LAST
-#define BP_SKIP_LAST 1  // the last iteration's (unread) message update is not computed
-#endif
-#ifndef BP_FIRST_SWEEP
-#define BP_FIRST_SWEEP 1  // first sweep (all tov 0): one fast_tanh per variable instead of per edge
-#endif
-#ifndef BP_SWEEP_TEST
-#define BP_SWEEP_TEST 1  // one short-division test per sweep (on the V->C arguments) instead of per group
-#endif
-[[maybe_unused]] constexpr double kClip2 = 2.0 * 4.97;  // exact: twice fast_tanh's clip bound
-#ifndef BP_GRID_CUS
-#define BP_GRID_CUS 256  // CUs the persistent grid covers (experiments only)
-#endif
+// Fixed kernel shape (round 3: the build-time experiment switches of round 2 are gone; DESIGN.md
+// section 3 lists what each alternative measured, and the fault one of them caused).  Divisions are
+// interleaved three at a time: a variable's three edges, and the nine edge slots of the edge-major
+// phase in three groups.  A group size that does not divide kEdgeSlots indexes past the lane's
+// register arrays -- undefined behaviour, which the compiler answers by deleting the divisions -- so
+// it is pinned and asserted here.
+constexpr int kDivGroup = 3;
+static_assert(kEdgeSlots % kDivGroup == 0 && kVarSlots == kDivGroup, "division groups tile the slots exactly");
+constexpr int kProdGroup = 3;  // check products between scheduling fences (register pressure)
+static_assert(kEdgeSlots % kProdGroup == 0, "product groups tile the edge slots");
+// Resident waves per SIMD the persistent grid is sized for.  The compiler is given a 3-wave register
+// budget: under a 4-wave budget (128 VGPRs) the allocator spills ~50 VGPRs of the fused sweep to
+// scratch, while under the 3-wave budget it needs only 123 -- which still leaves 4 waves resident
+// per SIMD (512 / 128).
+constexpr int kBpWavesPerSimd = 4;
+constexpr int kBpLbWaves = 3;
+constexpr int kBpGridCus = 256;        // MI355X: 256 CUs
+constexpr double kClip2 = 2.0 * 4.97;  // exact: twice fast_tanh's clip bound
 
 // LDS address-space view of a byte address (the product-factor reads compute raw LDS addresses)
 typedef __attribute__((address_space(3))) const double lds_f64;
@@ -338,7 +326,7 @@ struct BpArgs {
   double* llr_out;
   uint8_t* plain_out;
   ft8_result* res;
-  unsigned* work;
+  unsigned* work;             // [claim counter, retired waves], both 0 between launches
   unsigned long long* stats;  // nullable: [candidates, iterations entered, message passes, converged]
   int slot0;
   int tie_blocks;             // k_llr's first tie_blocks workgroups run tie_order
@@ -470,32 +458,7 @@ __device__ double pairwise174(const double* x, double* part, int lane) {
   return __shfl(tot, 0);
 }
 
-template <typename T>
-__device__ void extract_llr(const BpArgs& a, const T* wf, int at, int af, double* c, int lane) {
-  // ft8_extract_likelihood (ft8_decode.py:164-188)
-  if (lane < 58) {
-    const int k = lane;
-    const int sym = k + (k < 29 ? 7 : 14);
-    const int block = floordiv(at, a.sps) + sym;
-    double l0 = 0.0, l1 = 0.0, l2 = 0.0;
-    if (!(block < 0 || block >= a.num_blocks)) {
-      const T* row = wf + (int64_t)(at + sym * a.sps) * a.F + af;
-      double s[8], s2[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) s[i] = (double)row[i * a.bpt];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) s2[j] = s[kGrayD[j]];
-      l0 = pymax4(s2[4], s2[5], s2[6], s2[7]) - pymax4(s2[0], s2[1], s2[2], s2[3]);
-      l1 = pymax4(s2[2], s2[3], s2[6], s2[7]) - pymax4(s2[0], s2[1], s2[4], s2[5]);
-      l2 = pymax4(s2[1], s2[3], s2[5], s2[7]) - pymax4(s2[0], s2[2], s2[4], s2[6]);
-    }
-    c[3 * k] = l0;
-    c[3 * k + 1] = l1;
-    c[3 * k + 2] = l2;
-  }
-}
-
-// The same with the gathers spread over the wave: lane 8 g + i fetches tone i of symbol 8 r + g in
+// ft8_extract_likelihood (ft8_decode.py:164-188) with the gathers spread over the wave: lane 8 g + i fetches tone i of symbol 8 r + g in
 // round r, so one load instruction covers 8 symbols' rows (one or two cache lines each) instead of
 // 58 rows -- a candidate costs ~8x fewer L1 tag lookups -- and the tone powers reach their symbol's
 // lane through LDS (stage: 64 symbols x 8 tones).
@@ -537,10 +500,6 @@ __device__ void extract_llr_coop(const BpArgs& a, const T* wf, int at, int af, d
   }
 }
 
-#ifndef LLR_COOP
-#define LLR_COOP 1
-#endif
-
 // ---- k_llr: one wave per candidate -> normalised LLRs in global memory ---------------------------
 // modes: 0 per-slot candidate lists (skips ranks >= the slot's count), 1 explicit (slot, t, f) list,
 // 2 normalise given LLRs
@@ -577,12 +536,8 @@ __global__ __launch_bounds__(kWave) void k_llr(BpArgs a) {
   if (a.mode == 2) {
     for (int n = lane; n < FT8_LDPC_N; n += kWave) c[n] = a.llr_in[(int64_t)item * FT8_LDPC_N + n];
   } else {
-#if LLR_COOP
     __shared__ T stage[64 * 8];
     extract_llr_coop<T>(a, reinterpret_cast<const T*>(a.wf) + (int64_t)slot * a.T * a.F, at, af, c, stage, lane);
-#else
-    extract_llr<T>(a, reinterpret_cast<const T*>(a.wf) + (int64_t)slot * a.T * a.F, at, af, c, lane);
-#endif
   }
   __syncthreads();
   if (a.normalize) {  // ftx_normalize_logl (ft8_decode.py:190-198)
@@ -603,16 +558,7 @@ __global__ __launch_bounds__(kWave) void k_llr(BpArgs a) {
 // Phase boundary inside a sweep.  The workgroup is one wave and the LDS executes a wave's
 // instructions in order, so a later ds_read sees every earlier ds_write of the wave without
 // s_waitcnt / s_barrier; only the compiler must not move LDS accesses across the boundary.
-#ifndef BP_HW_BARRIER
-#define BP_HW_BARRIER 0
-#endif
-__device__ __forceinline__ void sweep_sync() {
-#if BP_HW_BARRIER
-  __syncthreads();
-#else
-  asm volatile("" ::: "memory");
-#endif
-}
+__device__ __forceinline__ void sweep_sync() { asm volatile("" ::: "memory"); }
 
 // np.clip(T, -2 c, 2 c) of fast_tanh's argument in the folded form (c = 4.97); NaN stays NaN when
 // the candidate has NaN inputs (nan_in, wave-uniform)
@@ -664,7 +610,7 @@ __device__ __forceinline__ float min3_abs_hi(double a, double b, double c) {
   return m;
 }
 
-// Per-sweep short-division test (BP_SWEEP_TEST): true when every V->C argument y of the wave
+// Per-sweep short-division test: true when every V->C argument y of the wave
 // (3 x 3 per lane, after np.clip) has |y| >= 2^-100 -- or is NaN, which either division path
 // turns into the same NaN (see div_rn).  That one test admits both phases' short divisions:
 //   * fast_tanh: |A| = |y| (15120 + z (420 + z)) >= 2^-100 * 15120 > 2^-480 (tanh_group's test);
@@ -739,7 +685,7 @@ __device__ __forceinline__ void check_products(double* x, uint32_t la, int lane)
 // ---- k_bp: persistent waves, one candidate at a time ----------------------------------------------
 // modes: 0 per-slot candidate lists (records carry slot / abs_time / abs_freq / score), 2 plain LLRs
 template <bool NANSAFE>
-__global__ __launch_bounds__(kWave, BP_LB_WAVES) void k_bp(BpArgs a) {
+__global__ __launch_bounds__(kWave, kBpLbWaves) void k_bp(BpArgs a) {
   __shared__ WaveLds L;
   const int lane = threadIdx.x;
   WaveTables tb;
@@ -761,10 +707,15 @@ __global__ __launch_bounds__(kWave, BP_LB_WAVES) void k_bp(BpArgs a) {
     // wave-uniform: candidate metadata then lives in SGPRs (scalar loads), not VGPRs
     item = __builtin_amdgcn_readfirstlane(__shfl(item, 0));
     if ((int)item >= a.n_items) {
-      // every wave's claims end with exactly one ticket >= n_items, so the wave holding the last
-      // ticket (n_items + waves - 1) claims after everyone else: it leaves the counter at 0 for the
-      // next launch (no memset kernel per launch; a fresh counter buffer is zeroed once, capi.hip)
-      if (lane == 0 && item == (unsigned)a.n_items + gridDim.x - 1u) atomicExch(a.work, 0u);
+      // every wave's claims end with exactly one ticket >= n_items, after which it retires: the wave
+      // whose retirement comes last (work[1] reaches gridDim - 1) runs after every other claim and
+      // leaves both counters at 0 for the next launch -- no memset kernel per launch (a fresh
+      // counter buffer is zeroed once, capi.hip), and whatever value the claim counter ended at,
+      // e.g. after a launch that was cut short, the next completed launch resets it
+      if (lane == 0 && atomicAdd(a.work + 1, 1u) == gridDim.x - 1u) {
+        atomicExch(a.work, 0u);
+        atomicExch(a.work + 1, 0u);
+      }
       break;
     }
 
@@ -822,7 +773,7 @@ __global__ __launch_bounds__(kWave, BP_LB_WAVES) void k_bp(BpArgs a) {
       // (A) variable-major: the hard decision and the three clipped variable->check arguments of
       // each of the lane's variables, kept in registers (no LDS store, so no phase boundary)
       double y[kVarSlots][3];
-      const bool sweep0 = BP_FIRST_SWEEP && iter == 0;
+      const bool sweep0 = iter == 0;
       if (sweep0) {
         // every tov is 0: messages = codeword + 0.0 (ldpc_decoder.py:72-73), and the argument of
         // each of a variable's edges is (c + 0.0) + 0.0 == c + 0.0
@@ -882,7 +833,7 @@ __global__ __launch_bounds__(kWave, BP_LB_WAVES) void k_bp(BpArgs a) {
       }
       // the last iteration's message update (ldpc_decoder.py:88-108) is never read: the loop ends
       // after it and the result is the plain / min_errors formed above
-      if (BP_SKIP_LAST && iter + 1 == a.max_iterations) break;
+      if (iter + 1 == a.max_iterations) break;
       // (C) variable -> check messages: toc = fast_tanh(-Tnm / 2), three interleaved divisions at a
       // time.  From y = -2 x (x the reference's clipped argument): with z = RN(y y) = 4 RN(x x),
       // every step of fast_tanh's polynomials (ldpc_decoder.py:11-20) is the reference's step scaled
@@ -895,7 +846,7 @@ __global__ __launch_bounds__(kWave, BP_LB_WAVES) void k_bp(BpArgs a) {
       // variable-major, straight from phase A's registers into each edge's slot
       static_assert(kDivGroup == 3 && kVarSlots == 3, "a division group is one variable's edges");
       // wave-uniform int (a bool crossing blocks would be kept as a VALU lane mask)
-      int fast = __builtin_amdgcn_readfirstlane(BP_SWEEP_TEST && sweep_fast(y) ? 1 : 0);
+      int fast = __builtin_amdgcn_readfirstlane(sweep_fast(y) ? 1 : 0);
       asm volatile("" : "+s"(fast));  // opaque SGPR: branches test it with s_cmp
       if (sweep0) {  // one fast_tanh per variable
         double v[kVarSlots] = {y[0][0], y[1][0], y[2][0]};
@@ -1031,6 +982,80 @@ __global__ __launch_bounds__(kWave) void k_compact(const ft8_result* res, const 
   if (lane == 0) counts[slot] = base;
 }
 
+// ---- k_pack: a batch's decodes -> one all-gather send buffer (ft8_pack_decodes) -------------------
+// One 1024-thread workgroup: the batch's slots in chunks of 1024, each chunk's capped counts turned
+// into row offsets by a block scan, then every thread of the block copies rows of the chunk (a row's
+// slot found by binary search over the offsets), so a slot with many decodes is not one thread's
+// serial copy.  Records are 40 B; a batch holds ~1-30 decodes per slot, so this is a few KB.
+constexpr int kPackThreads = 1024;
+__global__ __launch_bounds__(kPackThreads) void k_pack(const ft8_result* rec, const int32_t* counts, int n_slots,
+                                                       int cap, int capacity, int slot_offset, uint8_t* send,
+                                                       ft8_result* overflow) {
+  __shared__ int s_off[kPackThreads];
+  __shared__ int s_wave[kPackThreads / kWave + 1];
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid >> 6;
+  int32_t* cnt_out = reinterpret_cast<int32_t*>(send + 8);
+  ft8_result* rows = reinterpret_cast<ft8_result*>(send + pack_header_bytes(n_slots));
+  int carry = 0;
+  for (int base = 0; base < n_slots; base += kPackThreads) {
+    const int s = base + tid;
+    int c = 0;
+    if (s < n_slots) {
+      const int raw = counts[s];
+      cnt_out[s] = raw;
+      c = min(max(raw, 0), cap);
+    }
+    // exclusive scan of c over the block: wave scans, then the wave totals
+    int x = c;
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+      const int y = __shfl_up(x, o);
+      if (lane >= o) x += y;
+    }
+    if (lane == kWave - 1) s_wave[w] = x;
+    __syncthreads();
+    if (tid == 0) {
+      int acc = 0;
+      for (int i = 0; i < kPackThreads / kWave; ++i) {
+        const int t = s_wave[i];
+        s_wave[i] = acc;
+        acc += t;
+      }
+      s_wave[kPackThreads / kWave] = acc;
+    }
+    __syncthreads();
+    // slots past n_slots get an offset past every row, so the search below never lands on them
+    s_off[tid] = s < n_slots ? s_wave[w] + x - c : 0x7fffffff;
+    const int ct = s_wave[kPackThreads / kWave];
+    __syncthreads();
+    for (int r = tid; r < ct; r += kPackThreads) {
+      // the last slot whose first row is <= r: zero-count slots share the next slot's offset, so
+      // this is the slot holding row r
+      int lo = 0, hi = min(kPackThreads, n_slots - base) - 1;
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (s_off[mid] <= r) lo = mid;
+        else hi = mid - 1;
+      }
+      ft8_result v = rec[(int64_t)(base + lo) * cap + (r - s_off[lo])];
+      v.slot += slot_offset;
+      const int dst = carry + r;
+      if (dst < capacity) rows[dst] = v;
+      else if (overflow) overflow[dst - capacity] = v;
+    }
+    carry += ct;
+    __syncthreads();
+  }
+  // zero the unused rows (the exchange moves them; keep them deterministic)
+  for (int r = carry + tid; r < capacity; r += kPackThreads) {
+    uint64_t* p = reinterpret_cast<uint64_t*>(rows + r);
+#pragma unroll
+    for (int i = 0; i < (int)(sizeof(ft8_result) / 8); ++i) p[i] = 0;
+  }
+  for (int i = n_slots + tid; i < (int)((pack_header_bytes(n_slots) - 8) / 4); i += kPackThreads) cnt_out[i] = 0;
+  if (tid == 0) *reinterpret_cast<int64_t*>(send) = carry;
+}
+
 __global__ void k_crc14(const uint8_t* msg, const int32_t* nbits, int n, uint16_t* crc) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -1104,8 +1129,8 @@ hipError_t launch_bp(const BpLaunch& L, hipStream_t s) {
   if (L.n_items <= 0) return hipSuccess;
   BpArgs a = make_args(L);
   // L.work is 0 here: zeroed when its buffer was allocated, and every k_bp launch leaves it at 0
-  const int per_simd = max(1, min(L.grid_waves, BP_WAVES_PER_EU));
-  const int waves = min(L.n_items, BP_GRID_CUS * 4 * per_simd);  // resident waves, persistent
+  const int per_simd = max(1, min(L.grid_waves, kBpWavesPerSimd));
+  const int waves = min(L.n_items, kBpGridCus * 4 * per_simd);  // resident waves, persistent
   if (L.mode == 0) hipLaunchKernelGGL(k_bp<false>, dim3(waves), dim3(kWave), 0, s, a);
   else hipLaunchKernelGGL(k_bp<true>, dim3(waves), dim3(kWave), 0, s, a);
   return hipGetLastError();
@@ -1121,6 +1146,14 @@ hipError_t launch_compact(const CompactLaunch& L, hipStream_t s) {
   if (L.n_slots <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_compact, dim3(L.n_slots), dim3(kWave), 0, s, L.res, L.cand_count, L.N, L.out,
                      L.counts, L.cap, L.warn, L.tie);
+  return hipGetLastError();
+}
+
+hipError_t launch_pack(const ft8_result* rec, const int32_t* counts, int n_slots, int cap, int capacity,
+                       int slot_offset, uint8_t* send, ft8_result* overflow, hipStream_t s) {
+  static_assert(sizeof(ft8_result) % 8 == 0, "records are copied as 8-byte words");
+  hipLaunchKernelGGL(k_pack, dim3(1), dim3(kPackThreads), 0, s, rec, counts, n_slots, cap, capacity, slot_offset,
+                     send, overflow);
   return hipGetLastError();
 }
 

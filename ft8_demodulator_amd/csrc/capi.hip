@@ -520,7 +520,8 @@ int decode_pass(ft8_ctx* c, const void* d_samples, int dtype, int64_t n_samples,
   const int csz = (c->n_streams > 0 && c->chunk_slots > 0) ? c->chunk_slots : n_slots;
   const int n_chunks = (n_slots + csz - 1) / csz;
   const int n_str = (c->n_streams > 0 && n_chunks > 1) ? std::min(c->n_streams, n_chunks) : 0;
-  if ((rc = ensure_zeroed(c, c->work, sizeof(unsigned) * (size_t)std::max(n_chunks, 4), s))) return rc;
+  // k_bp counter pairs: [0, 1] belong to ft8_bp (a caller stream), [2 + 2k, 3 + 2k] to chunk k
+  if ((rc = ensure_zeroed(c, c->work, sizeof(unsigned) * 2 * (size_t)(n_chunks + 1), s))) return rc;
   hipError_t e = hipSuccess;
   if (n_str > 0) {
     while ((int)c->streams.size() < n_str) {
@@ -576,9 +577,9 @@ int decode_pass(ft8_ctx* c, const void* d_samples, int dtype, int64_t n_samples,
     B.llr_out = (double*)c->llr.p + (size_t)FT8_LDPC_N * c0 * N;
     B.llr_in = B.llr_out;
     B.res = (ft8_result*)c->res_all.p + (size_t)c0 * N;
-    B.work = (unsigned*)c->work.p + k;
+    B.work = (unsigned*)c->work.p + 2 + 2 * k;
     B.stats = (unsigned long long*)c->stats.p;
-    B.grid_waves = n_str > 0 ? c->bp_waves : 8;  // clamped to the kernel's BP_WAVES_PER_EU
+    B.grid_waves = n_str > 0 ? c->bp_waves : 8;  // clamped to the kernel's 4 resident waves per SIMD
     B.tie = tie;
     B.warn = warn;
     StageTimer t6(c, 6, cs);
@@ -965,7 +966,7 @@ int ft8_bp(ft8_ctx* c, const double* d_llr, int32_t n, int32_t max_iterations, u
   if (n <= 0) return FT8_OK;
   DeviceGuard dg(c->device);
   int rc;
-  if ((rc = ensure_zeroed(c, c->work, 16, (hipStream_t)stream))) return rc;
+  if ((rc = ensure_zeroed(c, c->work, 16, (hipStream_t)stream))) return rc;  // counters [0, 1]: ft8_bp's own
   BpLaunch L{};
   L.mode = 2;
   L.llr_in = d_llr;
@@ -1227,6 +1228,23 @@ int ft8_set_pipeline(ft8_ctx* c, int32_t chunk_slots, int32_t n_streams, int32_t
   c->n_streams = n_streams;
   c->bp_waves = bp_waves_per_simd;
   return FT8_OK;
+}
+
+int64_t ft8_pack_bytes(int32_t n_slots, int32_t capacity) {
+  if (n_slots < 0 || capacity < 0) return -1;
+  return pack_header_bytes(n_slots) + (int64_t)capacity * (int64_t)sizeof(ft8_result);
+}
+
+int ft8_pack_decodes(ft8_ctx* c, const ft8_result* d_records, const int32_t* d_counts, int32_t n_slots, int32_t cap,
+                     int32_t capacity, int32_t slot_offset, void* d_send, ft8_result* d_overflow, void* stream) {
+  if (!c || !d_send || n_slots < 0 || cap < 0 || capacity < 0) return fail(c, FT8_E_ARG, "bad argument");
+  if (n_slots > 0 && (!d_counts || (cap > 0 && !d_records))) return fail(c, FT8_E_ARG, "null records or counts");
+  if ((int64_t)n_slots * cap > INT32_MAX) return fail(c, FT8_E_RANGE, "n_slots * cap exceeds 2^31 rows");
+  if (((uintptr_t)d_send & 7) || ((uintptr_t)d_overflow & 7)) return fail(c, FT8_E_ARG, "buffers must be 8-byte aligned");
+  DeviceGuard dg(c->device);
+  hipError_t e = launch_pack(d_records, d_counts, n_slots, cap, capacity, slot_offset, (uint8_t*)d_send, d_overflow,
+                             (hipStream_t)stream);
+  return e == hipSuccess ? FT8_OK : hipfail(c, e, "pack launch");
 }
 
 int ft8_select_warnings(ft8_ctx* c, int32_t* d_out, int32_t n_slots, void* stream) {

@@ -148,10 +148,10 @@ struct BpLaunch {
   double* llr_out;         // k_llr output [n_items][174]
   uint8_t* plain_out;      // nullable [n_items][174]
   ft8_result* res;         // nullable [n_items]
-  unsigned* work;          // work counter (zeroed by the launcher)
+  unsigned* work;          // k_bp: 2 counters [claim, retired], 0 between launches (k_bp resets them)
   unsigned long long* stats = nullptr;  // [candidates, iterations entered, message passes, converged]
   int slot0 = 0;           // batch index of slot 0 (records carry slot0 + local slot)
-  int grid_waves = 4;      // k_bp persistent grid: resident waves per SIMD (<= BP_WAVES_PER_EU)
+  int grid_waves = 4;      // k_bp persistent grid: resident waves per SIMD (clamped to 4)
   // mode 0, nullable: slots whose order of equal scores k_select deferred (warn bit 3) get it
   // replayed by k_llr's first workgroups
   int32_t* tie = nullptr;  // [n_slots][tie_stride(N)]
@@ -171,6 +171,11 @@ struct CompactLaunch {
   const int32_t* tie = nullptr;
 };
 hipError_t launch_compact(const CompactLaunch& a, hipStream_t s);
+
+// ft8_pack_decodes (bp.hip): one workgroup packs a batch's decodes for the all-gather
+inline __host__ __device__ int64_t pack_header_bytes(int n_slots) { return 8 + ((4 * (int64_t)n_slots + 7) & ~7ll); }
+hipError_t launch_pack(const ft8_result* rec, const int32_t* counts, int n_slots, int cap, int capacity,
+                       int slot_offset, uint8_t* send, ft8_result* overflow, hipStream_t s);
 
 // ---- transmit chain + subtraction (tx.hip, subtract.hip) -------------------------------------
 struct SynthLaunch {

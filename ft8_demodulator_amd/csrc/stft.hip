@@ -26,9 +26,6 @@ namespace ft8 {
 namespace {
 
 constexpr int kThreads = 256;
-#ifndef STFT_PACKED
-#define STFT_PACKED 1  // the production geometry runs stft3840.hip's packed kernel
-#endif
 
 template <typename T>
 __device__ __forceinline__ cplx<T> cadd(cplx<T> a, cplx<T> b) { return {a.x + b.x, a.y + b.y}; }
@@ -420,245 +417,6 @@ __global__ __launch_bounds__(kThreads, (MAXV <= 16 ? 2 : 1)) void k_stft(StftArg
   }
 }
 
-// ---- k_stft3840: the production geometry (real input, nfft = 3840, nperseg = 1920, hop = 960) --
-// 12 kHz with bins_per_tone = steps_per_symbol = 2.  The half-length complex FFT has P = 1920 =
-// 16 x 8 x 15 points: three Stockham stages with compile-time radices and strides, one butterfly
-// per thread per stage (128 threads; stage 2 runs two), ping-pong LDS buffers, twiddles held in
-// registers (each thread always owns the same butterfly columns).  A workgroup walks a run of
-// consecutive frames of one slot: a frame's second half is the next frame's first half, so each
-// thread keeps its raw samples in registers and loads only the 4 new pairs per frame (a run of c
-// frames reads (c + 1) / c of its samples), prefetching the next frame while the current one is
-// transformed.
-constexpr int k38P = 1920;
-constexpr int k38Threads = 128;
-// frames per workgroup: 8 gives 24 workgroups per slot, which fills the CUs more evenly than 16
-// (per 256-slot step: 16 -> 0.250 ms, 12 -> 0.240, 8 -> 0.233, 6 -> 0.232, 4 -> 0.239)
-constexpr int k38Chunk = 8;
-
-__device__ __forceinline__ cplx<float> w16(int m) {  // exp(-2 pi i m / 16), m in [0, 9]
-  constexpr float c[10] = {1.0f, 0.92387953251128675613f, 0.70710678118654752440f, 0.38268343236508977173f,
-                           0.0f, -0.38268343236508977173f, -0.70710678118654752440f, -0.92387953251128675613f,
-                           -1.0f, -0.92387953251128675613f};
-  constexpr float sn[10] = {0.0f, -0.38268343236508977173f, -0.70710678118654752440f, -0.92387953251128675613f,
-                            -1.0f, -0.92387953251128675613f, -0.70710678118654752440f, -0.38268343236508977173f,
-                            0.0f, 0.38268343236508977173f};
-  return {c[m], sn[m]};
-}
-
-// 16-point DFT of x[0..7] with x[8..15] = 0 (4 x 4 Cooley-Tukey), y in natural order
-__device__ __forceinline__ void dft16_half(const cplx<float>* x, cplx<float>* y) {
-  cplx<float> A[4][4];  // [n2][k1]
-#pragma unroll
-  for (int n2 = 0; n2 < 4; ++n2) {
-    const cplx<float> a = x[n2], b = x[4 + n2];
-    A[n2][0] = cadd(a, b);
-    A[n2][1] = cadd(a, mul_mi(b));
-    A[n2][2] = csub(a, b);
-    A[n2][3] = csub(a, mul_mi(b));
-  }
-#pragma unroll
-  for (int n2 = 1; n2 < 4; ++n2)
-#pragma unroll
-    for (int k1 = 1; k1 < 4; ++k1) A[n2][k1] = cmul(A[n2][k1], w16(n2 * k1));
-#pragma unroll
-  for (int k1 = 0; k1 < 4; ++k1) {
-    cplx<float> v[4] = {A[0][k1], A[1][k1], A[2][k1], A[3][k1]};
-    Dft<4, float>::run(v);
-#pragma unroll
-    for (int k2 = 0; k2 < 4; ++k2) y[k1 + 4 * k2] = v[k2];
-  }
-}
-
-// 15-point DFT, prime-factor 3 x 5 (no internal twiddles): n = (5 n1 + 3 n2) mod 15,
-// k = (10 k1 + 6 k2) mod 15
-__device__ __forceinline__ void dft15(const cplx<float>* x, cplx<float>* y) {
-  cplx<float> Y[3][5];
-#pragma unroll
-  for (int n1 = 0; n1 < 3; ++n1) {
-#pragma unroll
-    for (int n2 = 0; n2 < 5; ++n2) Y[n1][n2] = x[(5 * n1 + 3 * n2) % 15];
-    Dft<5, float>::run(Y[n1]);
-  }
-#pragma unroll
-  for (int k2 = 0; k2 < 5; ++k2) {
-    cplx<float> v[3] = {Y[0][k2], Y[1][k2], Y[2][k2]};
-    Dft<3, float>::run(v);
-#pragma unroll
-    for (int k1 = 0; k1 < 3; ++k1) y[(10 * k1 + 6 * k2) % 15] = v[k1];
-  }
-}
-
-template <typename InT>
-__device__ __forceinline__ void load_pair(const InT* x, int64_t n0, float& a, float& b) {
-  if constexpr (sizeof(InT) == 4) {
-    const float2 v = *reinterpret_cast<const float2*>(x + n0);
-    a = v.x;
-    b = v.y;
-  } else {
-    const short2 v = *reinterpret_cast<const short2*>(x + n0);
-    a = (float)v.x / 32767.0f;  // read_wave_file: float32(x) / iinfo(int16).max
-    b = (float)v.y / 32767.0f;
-  }
-}
-
-template <typename InT>
-__global__ __launch_bounds__(k38Threads) void k_stft3840(StftArgs a) {
-  // bufA is read and written with pidx padding: the stage-1 writes go out with a 16-complex stride
-  // across lanes (128 B: 32-way bank conflicts unpadded)
-  __shared__ cplx<float> bufA[k38P + k38P / 16 + 1];
-  __shared__ cplx<float> bufB[k38P];
-  const int t = threadIdx.x;
-  const int chunks = (a.nt_out + k38Chunk - 1) / k38Chunk;
-  const int slot = blockIdx.x / chunks;
-  const int c = blockIdx.x - slot * chunks;
-  const int f_begin = c * k38Chunk, f_end = min(a.nt_out, f_begin + k38Chunk);
-  const cplx<float>* tw = reinterpret_cast<const cplx<float>*>(a.tw);            // W_1920^m
-  const cplx<float>* post = reinterpret_cast<const cplx<float>*>(a.post);  // W_3840^k
-  const float* win = reinterpret_cast<const float*>(a.window);
-  // twiddle seeds (registers): stage 2 W_128^k (k = t % 16), stage 3 W_1920^t, epilogue
-  // W_3840^(f_lo + t) and its 128-bin step; the powers are formed by complex recurrence each frame
-  // (relative error ~15 ulp, far inside the dB tolerance)
-  cplx<float> s2 = tw[15 * (t & 15)], s3 = tw[t];
-  const bool rec_post = a.f_lo + a.nf_out <= k38P;
-  const bool full = a.f_lo == 0 && a.nf_out == k38P;  // every f >= 0 bin kept (no band mask)
-  // 10 log10(v) = (10 log10 2) log2(v): v_log_f32 on a normal argument (v >= 1e-12)
-  constexpr float kDb = 3.0102999566398119521f;
-  cplx<float> p0 = post[min(a.f_lo + t, k38P)];
-  const cplx<float> pstep = post[k38Threads];
-
-  // per-thread constants: the window of its 8 stage-1 pairs (twiddles come from the L1-resident table)
-  const bool s1 = t < 120;
-  float w0[8], w1[8];
-#pragma unroll
-  for (int r = 0; r < 8; ++r) {
-    const int n = t + 120 * r;
-    w0[r] = s1 ? win[2 * n] : 0.0f;
-    w1[r] = s1 ? win[2 * n + 1] : 0.0f;
-  }
-
-  const InT* xs = reinterpret_cast<const InT*>(a.samples) + (int64_t)slot * a.slot_stride;
-  float ra[8], rb[8];  // raw pairs (x[2n], x[2n+1]), n = t + 120 r, of the current frame
-  {
-    const int64_t base = (int64_t)(a.t_lo + f_begin) * 960;
-#pragma unroll
-    for (int r = 0; r < 8; ++r)
-      if (s1) load_pair<InT>(xs, base + 2 * (t + 120 * r), ra[r], rb[r]);
-  }
-  const float scale = (float)a.scale;
-  float* outb = reinterpret_cast<float*>(a.out);
-  for (int f = f_begin; f < f_end; ++f) {
-    // re-opaque the seeds so the per-frame twiddle powers are not hoisted into ~50 live registers
-    asm volatile("" : "+v"(s2.x), "+v"(s2.y), "+v"(s3.x), "+v"(s3.y), "+v"(p0.x), "+v"(p0.y));
-    // prefetch the next frame's 4 new pairs (n + 480 = t + 120 (r + 4))
-    float na[4], nb[4];
-    const bool more = f + 1 < f_end;
-    if (s1 && more) {
-      const int64_t base = (int64_t)(a.t_lo + f + 1) * 960;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) load_pair<InT>(xs, base + 2 * (t + 120 * (r + 4)), na[r], nb[r]);
-    }
-    // stage 1: radix 16, Ns = 1: inputs z[t + 120 r] (r >= 8 is zero padding) -> bufA[16 t + k]
-    __syncthreads();  // the previous frame's epilogue has finished reading bufA
-    if (s1) {
-      cplx<float> z[8], y[16];
-#pragma unroll
-      for (int r = 0; r < 8; ++r) z[r] = {w0[r] * ra[r], w1[r] * rb[r]};
-      dft16_half(z, y);
-#pragma unroll
-      for (int k = 0; k < 16; ++k) bufA[pidx(16 * t + k)] = y[k];
-    }
-    __syncthreads();
-    // stage 2: radix 8, Ns = 16: j in {t, t + 128} (j < 240)
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int j = t + 128 * h;
-      if (j < 240) {
-        cplx<float> v[8];
-#pragma unroll
-        for (int r = 0; r < 8; ++r) v[r] = bufA[pidx(j + 240 * r)];
-        if ((j & 15) != 0) {
-          cplx<float> w = s2;  // W_128^(r k)
-#pragma unroll
-          for (int r = 1; r < 8; ++r) {
-            v[r] = cmul(v[r], w);
-            if (r < 7) w = cmul(w, s2);
-          }
-        }
-        Dft<8, float>::run(v);
-        const int d0 = (j >> 4) * 128 + (j & 15);
-#pragma unroll
-        for (int r = 0; r < 8; ++r) bufB[d0 + 16 * r] = v[r];
-      }
-    }
-    __syncthreads();
-    // stage 3: radix 15, Ns = 128: j = t -> natural order into bufA
-    {
-      cplx<float> v[15], y[15];
-#pragma unroll
-      for (int r = 0; r < 15; ++r) v[r] = bufB[t + 128 * r];
-      if (t != 0) {
-        cplx<float> w = s3;  // W_1920^(r t)
-#pragma unroll
-        for (int r = 1; r < 15; ++r) {
-          v[r] = cmul(v[r], w);
-          if (r < 14) w = cmul(w, s3);
-        }
-      }
-      dft15(v, y);
-#pragma unroll
-      for (int r = 0; r < 15; ++r) bufA[pidx(t + 128 * r)] = y[r];
-    }
-    __syncthreads();
-    // epilogue: real-signal spectrum, power, dB, kept bins
-    float* out = outb + ((int64_t)slot * a.nt_out + f) * a.nf_out;
-    if (full) {
-      // all bins [0, P): k and P - k share Z[k], Z[P - k] and, since W_N^(P-k) = -conj(W_N^k),
-      // X[P - k] = conj(s)/2 - i conj(W_N^k d)/2 from the same s = Z[k] + conj Z[P-k],
-      // d = Z[k] - conj Z[P-k]
-      cplx<float> pw_k = p0;  // W_3840^k, k = t + 128 j
-      for (int k = t; k <= k38P / 2; k += k38Threads) {
-        const cplx<float> A = bufA[pidx(k)];
-        const cplx<float> Bc = bufA[pidx(k == 0 ? 0 : k38P - k)];
-        const cplx<float> B = {Bc.x, -Bc.y};
-        const cplx<float> sm = cadd(A, B), df = csub(A, B);
-        const cplx<float> wd = cmul(pw_k, df);
-        pw_k = cmul(pw_k, pstep);
-        const float p1 = (0.25f * ((sm.x + wd.y) * (sm.x + wd.y) + (sm.y - wd.x) * (sm.y - wd.x))) * scale;
-        out[k] = kDb * __builtin_amdgcn_logf(1e-12f + p1);
-        if (k != 0 && k != k38P / 2) {
-          const float p2 = (0.25f * ((sm.x - wd.y) * (sm.x - wd.y) + (sm.y + wd.x) * (sm.y + wd.x))) * scale;
-          out[k38P - k] = kDb * __builtin_amdgcn_logf(1e-12f + p2);
-        }
-      }
-    } else {
-      cplx<float> pw_k = p0;  // W_3840^k for k = f_lo + i (recurrence over i += 128)
-      for (int i = t; i < a.nf_out; i += k38Threads) {
-        const int k = a.f_lo + i;
-        const int kk = (k <= k38P) ? k : 2 * k38P - k;
-        const cplx<float> A = bufA[pidx(kk == k38P ? 0 : kk)];
-        const cplx<float> Bc = bufA[pidx(kk == 0 ? 0 : k38P - kk)];
-        const cplx<float> B = {Bc.x, -Bc.y};
-        const cplx<float> sm = cadd(A, B), df = csub(A, B);
-        const cplx<float> wd = cmul(rec_post ? pw_k : post[kk], df);
-        pw_k = cmul(pw_k, pstep);
-        const cplx<float> X = {0.5f * (sm.x + wd.y), 0.5f * (sm.y - wd.x)};
-        const float pw = (X.x * X.x + X.y * X.y) * scale;
-        out[i] = kDb * __builtin_amdgcn_logf(1e-12f + pw);
-      }
-    }
-    // slide the window: pairs r >= 4 become r - 4, the prefetched pairs fill r = 4..7
-    if (more) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        ra[r] = ra[r + 4];
-        rb[r] = rb[r + 4];
-        ra[r + 4] = na[r];
-        rb[r + 4] = nb[r];
-      }
-    }
-  }
-}
-
 // ---- k_stftc3840: complex input, nfft = 3840, nperseg = 1920, hop = 240 M (M in 1, 2, 4, 8) -----
 // The beacon receiver's geometry (12 kHz complex baseband, frequency_correction.py; the reference
 // test runs steps_per_symbol = 8, hop 240).  P = 3840 = 16 x 16 x 15: 256 threads, one butterfly per
@@ -1031,18 +789,8 @@ hipError_t launch_stft(const StftLaunch& L, hipStream_t s) {
       default: return hipErrorInvalidValue;
     }
   }
-  // production geometry: 12 kHz, bins_per_tone = steps_per_symbol = 2 (pairs need an even stride)
-#if STFT_PACKED
+  // production geometry (12 kHz, bins_per_tone = steps_per_symbol = 2): stft3840.hip's packed kernel
   if (stft3840_eligible(L)) return launch_stft3840(L, s);
-#endif
-  if (!L.argmax && (L.dtype == FT8_F32 || L.dtype == FT8_I16) && L.nfft == 2 * k38P && L.nperseg == k38P && L.hop == 960 &&
-      a.P == k38P && (L.slot_stride % 2) == 0) {
-    const int chunks = (a.nt_out + k38Chunk - 1) / k38Chunk;
-    const dim3 grid((unsigned)(chunks * L.n_slots));
-    if (L.dtype == FT8_F32) hipLaunchKernelGGL(k_stft3840<float>, grid, dim3(k38Threads), 0, s, a);
-    else hipLaunchKernelGGL(k_stft3840<int16_t>, grid, dim3(k38Threads), 0, s, a);
-    return hipGetLastError();
-  }
   // complex input in the beacon receiver's geometry (12 kHz: nfft 3840, nperseg 1920, hop 240 M)
   if ((L.dtype == FT8_C64 || L.dtype == FT8_C128) && L.nfft == kC38P && L.nperseg == 1920 && a.P == kC38P &&
       (L.hop == 240 || L.hop == 480 || L.hop == 960 || L.hop == 1920)) {

@@ -194,20 +194,14 @@ __device__ __forceinline__ f2 load_pair(const InT* x, int64_t n0) {
 }
 
 constexpr int kP = 1920;
-#ifndef S38_ONEBUF
-#define S38_ONEBUF 0  // 1: one LDS buffer (every stage loads its inputs, barrier, stores): 16 KB per workgroup
-#endif
-#ifndef S38_THREADS
-#define S38_THREADS 256  // four waves per frame: stage 2 one butterfly per thread, stages 1 and 3 on the
-                         // first 120 / 128 threads, the epilogue on all (128: two waves, two stage-2
-                         // butterflies per thread; 0.185 vs 0.175 ms per 256-slot launch)
-#endif
-constexpr int kThreads38 = S38_THREADS;
-static_assert(kThreads38 == 128 || (kThreads38 == 256 && !S38_ONEBUF), "256 threads: two buffers");
-#ifndef S38_CHUNK
-#define S38_CHUNK 6  // 6: 0.168-0.171 ms vs 8: 0.172-0.178, 4/5/12/16 no better (profiles/r2_s27/s28_*_ab.log)
-#endif
-constexpr int kChunk = S38_CHUNK;  // frames per workgroup (31 workgroups per slot at 186 frames)
+// four waves per frame: stage 2 one butterfly per thread, stages 1 and 3 on the first 120 / 128
+// threads, the epilogue on all (two waves with two stage-2 butterflies per thread: 0.185 vs 0.175 ms
+// per 256-slot launch; one LDS buffer needs 176 VGPRs at 128 threads)
+constexpr int kThreads38 = 256;
+// frames per workgroup, 31 workgroups per slot at 186 frames (6: 0.168-0.171 ms vs 8: 0.172-0.178,
+// 4/5/12/16 no better, profiles/r2_s27/s28_*_ab.log)
+constexpr int kChunk = 6;
+static_assert(kThreads38 == 256 && kThreads38 >= 240, "stage 2: one radix-8 butterfly per thread (240)");
 
 struct Args {
   const void* samples;
@@ -222,22 +216,12 @@ struct Args {
 
 __device__ __forceinline__ int pidx(int i) { return i + (i >> 4); }
 
-#ifndef S38_WINREG
-#define S38_WINREG 1  // the thread's window values stay in registers (0: reloaded from L1 each frame)
-#endif
-
 template <typename InT>
 __global__ __launch_bounds__(kThreads38) void k_stft3840p(Args a) {
   // bufA is read and written with pidx padding: the stage-1 writes go out with a 16-complex stride
   // across lanes (128 B: 32-way bank conflicts unpadded)
   __shared__ f2 bufA[kP + kP / 16 + 1];
-#if S38_ONEBUF
-  f2* const bufB = bufA;
-#define S38_BIDX(i) pidx(i)
-#else
   __shared__ f2 bufB[kP];
-#define S38_BIDX(i) (i)
-#endif
   const int t = threadIdx.x;
   const int chunks = (a.nt_out + kChunk - 1) / kChunk;
   const int slot = blockIdx.x / chunks;
@@ -255,17 +239,11 @@ __global__ __launch_bounds__(kThreads38) void k_stft3840p(Args a) {
   const f2 pstep = a.post[kThreads38];
   const f2 qscale = splat(0.25f * a.scale);  // |2 X|^2 / 4 / (sum w)^2 (powers of two: exact)
 
-  // the window of the thread's 8 stage-1 pairs
+  // the window of the thread's 8 stage-1 pairs, in registers
   const bool s1 = t < 120;
-  auto window = [&](int r) -> f2 {
-    const int n = t + 120 * r;
-    return *reinterpret_cast<const f2*>(a.window + 2 * n);
-  };
-#if S38_WINREG
   f2 win[8];
 #pragma unroll
-  for (int r = 0; r < 8; ++r) win[r] = s1 ? window(r) : splat(0.0f);
-#endif
+  for (int r = 0; r < 8; ++r) win[r] = s1 ? *reinterpret_cast<const f2*>(a.window + 2 * (t + 120 * r)) : splat(0.0f);
   const InT* xs = reinterpret_cast<const InT*>(a.samples) + (int64_t)slot * a.slot_stride;
   f2 raw[8];  // raw pairs (x[2n], x[2n+1]), n = t + 120 r, of the current frame
   {
@@ -289,40 +267,19 @@ __global__ __launch_bounds__(kThreads38) void k_stft3840p(Args a) {
     if (s1) {
       f2 z[8], y[16];
 #pragma unroll
-#if S38_WINREG
       for (int r = 0; r < 8; ++r) z[r] = win[r] * raw[r];
-#else
-      for (int r = 0; r < 8; ++r) z[r] = window(r) * raw[r];
-#endif
       dft16_half(z, y);
 #pragma unroll
       for (int k = 0; k < 16; ++k) bufA[pidx(16 * t + k)] = y[k];
     }
     __syncthreads();
-    // stage 2: radix 8, Ns = 16: j in {t, t + 128} (j < 240); with 256 threads j = t
-#if S38_ONEBUF
-    f2 v2[2][8];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int j = t + 128 * h;
+    // stage 2: radix 8, Ns = 16: j = t (j < 240)
+    {
+      const int j = t;
       if (j < 240) {
-#pragma unroll
-        for (int r = 0; r < 8; ++r) v2[h][r] = bufA[pidx(j + 240 * r)];
-      }
-    }
-    __syncthreads();  // every stage-2 input is in registers before the buffer is overwritten
-#endif
-#pragma unroll
-    for (int h = 0; h < (kThreads38 == 256 ? 1 : 2); ++h) {
-      const int j = t + 128 * h;
-      if (j < 240) {
-#if S38_ONEBUF
-        f2* v = v2[h];
-#else
         f2 v[8];
 #pragma unroll
         for (int r = 0; r < 8; ++r) v[r] = bufA[pidx(j + 240 * r)];
-#endif
         if ((j & 15) != 0) {
           f2 w = s2;  // W_128^(r k)
 #pragma unroll
@@ -334,18 +291,15 @@ __global__ __launch_bounds__(kThreads38) void k_stft3840p(Args a) {
         dft8(v);
         const int d0 = (j >> 4) * 128 + (j & 15);
 #pragma unroll
-        for (int r = 0; r < 8; ++r) bufB[S38_BIDX(d0 + 16 * r)] = v[r];
+        for (int r = 0; r < 8; ++r) bufB[d0 + 16 * r] = v[r];
       }
     }
     __syncthreads();
     // stage 3: radix 15, Ns = 128: j = t -> natural order into bufA
-    if (kThreads38 == 128 || t < 128) {
+    if (t < 128) {
       f2 v[15], y[15];
 #pragma unroll
-      for (int r = 0; r < 15; ++r) v[r] = bufB[S38_BIDX(t + 128 * r)];
-#if S38_ONEBUF
-      __syncthreads();
-#endif
+      for (int r = 0; r < 15; ++r) v[r] = bufB[t + 128 * r];
       if (t != 0) {
         f2 w = s3;  // W_1920^(r t)
 #pragma unroll

@@ -173,44 +173,11 @@ __global__ void k_score_list(const T* wf, int Tn, int F, int sps, int bpt, const
 }
 
 // ---- k_score2 ----------------------------------------------------------------------------------
-#ifndef S2_LOADFIRST
-#define S2_LOADFIRST 0
-#endif
 constexpr int kS2TW = 128;                 // grid columns per workgroup (64 lanes x 2)
 constexpr int kS2R = 22;                   // grid rows per workgroup (88 = 4 x 22 at 12 kHz)
 constexpr int kS2Waves = 11;               // each wave takes rows w, w + 11
 constexpr int kS2Threads = kS2Waves * kWave;
 typedef float f32x2 __attribute__((ext_vector_type(2)));
-
-// The 25 differences of a Costas band in the reference order (ft8_decode.py:66-94: per symbol k,
-// tone-1, tone+1, time-1, time+1), as slots of a list of distinct (row, column) reads relative to
-// the band's first staged row (rows in steps_per_symbol, columns in bins_per_tone)
-struct BandPlan {
-  int nload;
-  int row[32], col[32];
-  int ctr[25], nbr[25];
-};
-constexpr BandPlan band_plan() {
-  BandPlan b{};
-  auto slot = [&b](int r, int c) {
-    for (int i = 0; i < b.nload; ++i)
-      if (b.row[i] == r && b.col[i] == c) return i;
-    b.row[b.nload] = r;
-    b.col[b.nload] = c;
-    return b.nload++;
-  };
-  int t = 0;
-  for (int k = 0; k < 7; ++k) {
-    const int tone = kCostasC[k], r = k + 1;
-    const int c = slot(r, tone);
-    if (tone > 0) { b.ctr[t] = c; b.nbr[t++] = slot(r, tone - 1); }
-    if (tone < 7) { b.ctr[t] = c; b.nbr[t++] = slot(r, tone + 1); }
-    if (k > 0) { b.ctr[t] = c; b.nbr[t++] = slot(r - 1, tone); }
-    if (k < 6) { b.ctr[t] = c; b.nbr[t++] = slot(r + 1, tone); }
-  }
-  return b;
-}
-static_assert(band_plan().nload == 30, "Costas band reads");
 
 template <int BPT, int SPS>
 struct S2Geom {
@@ -327,18 +294,6 @@ __global__ __launch_bounds__(kS2Threads) void k_score2(ScoreArgs a) {
       if (lo >= 0 && lo <= nb - 7) {
         // every symbol of the band and all its neighbours in range: straight-line code, so the
         // 35 loads issue together (25 differences, in the reference order)
-#if S2_LOADFIRST
-        // the band's distinct reads (30: two time neighbours are another symbol's frequency
-        // neighbour) all issue before the first difference
-        constexpr BandPlan bp = band_plan();
-        const float* bb = tb + m * H * P;
-        f32x2 v[bp.nload];
-#pragma unroll
-        for (int i = 0; i < bp.nload; ++i) v[i] = ld2<BPT>(bb + bp.row[i] * SPS * P + bp.col[i] * BPT);
-        asm volatile("" ::: "memory");
-#pragma unroll
-        for (int t = 0; t < 25; ++t) score += v[bp.ctr[t]] - v[bp.nbr[t]];
-#else
 #pragma unroll
         for (int k = 0; k < 7; ++k) {
           const int tone = kCostasC[k];
@@ -349,7 +304,6 @@ __global__ __launch_bounds__(kS2Threads) void k_score2(ScoreArgs a) {
           if (k > 0) score += pw - ld2<BPT>(rp - SPS * P);
           if (k < 6) score += pw - ld2<BPT>(rp + SPS * P);
         }
-#endif
         n += 25;
       } else if (lo + 6 >= 0 && lo < nb) {
         // a band crossing the waterfall's first or last block: the reference's per-term tests

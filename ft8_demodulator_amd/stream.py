@@ -21,7 +21,7 @@ from typing import Iterable, Iterator, List
 import numpy as np
 
 from . import _lib
-from ._pipeline import SlotDecoder, records_to_results
+from ._pipeline import SlotDecoder, records_to_results, warn_truncated
 
 
 class StreamDecoder:
@@ -108,7 +108,9 @@ class StreamDecoder:
         self.ready[i].synchronize()
         cap = self.dec.cap
         recs = self.hout[i][: nb * cap * _lib.RESULT_DTYPE.itemsize].numpy().view(_lib.RESULT_DTYPE).reshape(nb, cap)
-        cnt = np.minimum(self.hcnt[i][:nb].numpy(), cap)
+        raw = self.hcnt[i][:nb].numpy()
+        warn_truncated(raw, cap, stacklevel=3)
+        cnt = np.minimum(raw, cap)
         out = [[] for _ in range(nb)]
         # every decode of the batch converted in one call (slot-major, candidate order), then dealt
         sel = np.arange(cap)[None, :] < cnt[:, None]

@@ -190,6 +190,21 @@ int ft8_decode_batch(ft8_ctx* ctx, const void* d_samples, int dtype, int64_t n_s
  * next chunk's STFT/score measured no gain.  Results do not depend on the setting. */
 int ft8_set_pipeline(ft8_ctx* ctx, int32_t chunk_slots, int32_t n_streams, int32_t bp_waves_per_simd);
 
+/* ---- multi-GPU exchange (slot shards, one all-gather of the decodes per batch) --
+ * No reference counterpart (the reference is single-process).  Packs the decodes of one
+ * ft8_decode_batch (d_records[n_slots][cap], d_counts[n_slots]) into ONE byte buffer that a
+ * collective (RCCL all-gather) moves as-is, on the device and without a host sync:
+ *   d_send = [int64 total][int32 counts[n_slots], padded to 8 B][capacity x ft8_result]
+ * total = sum over slots of min(counts, cap) (counts are copied uncapped); records in slot order,
+ * then candidate order, each with ft8_result.slot += slot_offset (global slot ids); rows of the
+ * send buffer past total are zeroed.  Rows >= capacity go to d_overflow[row - capacity] when
+ * d_overflow (capacity for n_slots * cap - capacity rows) is non-null, else are dropped -- the
+ * receiver sees total > capacity either way.  ft8_pack_bytes gives the send-buffer size. */
+int64_t ft8_pack_bytes(int32_t n_slots, int32_t capacity);
+int ft8_pack_decodes(ft8_ctx* ctx, const ft8_result* d_records, const int32_t* d_counts, int32_t n_slots,
+                     int32_t cap, int32_t capacity, int32_t slot_offset, void* d_send, ft8_result* d_overflow,
+                     void* stream);
+
 /* Per-slot flags of the last selection (copied device->device into d_out[n_slots]):
  * bit 0: an exact score tie reached a heap comparison (the reference raises TypeError there,
  *        ftx_types.py:37-47; here ties are ordered by scan index), bit 1: unused (0), bit 2

@@ -8,7 +8,7 @@ from conftest import ROOT
 
 def _declared():
     src = open(os.path.join(ROOT, "include", "ft8hip.h")).read()
-    return sorted(set(re.findall(r"^(?:int|const char\*)\s+(ft8_\w+)\(", src, flags=re.M)))
+    return sorted(set(re.findall(r"^(?:int|int64_t|const char\*)\s+(ft8_\w+)\(", src, flags=re.M)))
 
 
 def test_header_symbols_exported():

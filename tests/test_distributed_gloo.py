@@ -1,5 +1,6 @@
 """N>1 path on CPU: world_size 2 over gloo -- slot sharding and the record all-gathers (fixed
-buffers, fixed-capacity compaction and the data-sized two-phase exchange)."""
+buffers; the packed exchange with a capacity below the total, whose overflow rows take the second
+exchange; a larger batch that grows the capacity; a step with no decodes)."""
 import os
 
 import numpy as np
@@ -34,7 +35,7 @@ def _worker(rank, world, port, n_slots, q):
         rec, cnt = _records(lo, hi, cap, torch.arange(lo, hi, dtype=torch.int32) % 4)
         r_all, c_all = gather_records(rec, cnt)
         d_all, dc_all, tot = gather_decodes(rec, cnt, cap, 4)
-        compact = [d_all[r, :min(int(tot[r]), 4), 0].tolist() for r in range(world)]
+        compact = [d_all[r, :int(tot[r]), 0].tolist() for r in range(world)]
         # data-sized exchange with many decodes per slot (rank 1: 10 + 11 + 12 + 12 rows > 8 per slot)
         cap2 = 12
         rec2, cnt2 = _records(lo, hi, cap2, torch.arange(lo, hi, dtype=torch.int32) + 6)
@@ -80,11 +81,11 @@ def test_gloo_world2_gather():
         assert zero == ([2, 0, 40], [[0, 0, 0, 0], [0, 0, 0, 0]], [0, 0], 0)
         assert recs == [[0, 1, 2, 3], [4, 5, 6, 7]]
         assert cnts == [[0, 1, 2, 3], [0, 1, 2, 3]]
-        # compacted: slot s contributes min(count, cap) rows tagged s, in slot order; rank 1 holds
-        # 0 + 1 + 2 + 3 = 6 decodes for a capacity of 4, so its total flags the truncation
+        # packed: slot s contributes min(count, cap) rows tagged s, in slot order; each rank holds
+        # 0 + 1 + 2 + 3 = 6 decodes for a capacity of 4, so rows 4 and 5 come by the overflow exchange
         assert dcnts == cnts
         assert tot == [0 + 1 + 2 + 3, 0 + 1 + 2 + 3]
-        assert compact == [[1, 2, 2, 3], [5, 6, 6, 7]]
+        assert compact == [[1, 2, 2, 3, 3, 3], [5, 6, 6, 7, 7, 7]]
         # sized: counts 6..13 clamped to cap 12 -> rank 0 holds 6+7+8+9 = 30 rows, rank 1 10+11+12+12 = 45;
         # the exchange carries exactly 45 rows per rank, nothing is truncated, slots are global
         shape, stot, slots, rows, tags = sized

@@ -10,11 +10,16 @@ from conftest import DATA
 pytestmark = pytest.mark.gpu
 
 
-def _same(got, gold, tag, atol=2e-3):
-    """Payload, CRC, status, time and frequency exact; score within the STFT tolerance (the GPU FFT
-    is not pocketfft: dB differences up to 1e-3 on strong bins move a 75-term mean by < atol)."""
+SCORE_ATOL = 1e-4  # end-to-end score tolerance of a decode on float32 input
+
+
+def _same(got, gold, tag, atol=SCORE_ATOL):
+    """Payload, CRC, status, time and frequency exact; score within `atol` (a scalar, or one value
+    per decode).  The GPU FFT is a float32 FFT like scipy's but not pocketfft, so a score differs by
+    its rounding; atol defaults to 1e-4 (float32 scores of strong candidates move by ~1e-6)."""
     assert [g[:7] + (g[8],) for g in got] == [r[:7] + (r[8],) for r in gold], tag
-    assert np.allclose([g[7] for g in got], [r[7] for r in gold], rtol=0, atol=atol), tag
+    d = np.abs(np.array([g[7] for g in got]) - np.array([r[7] for r in gold]))
+    assert np.all(d <= np.broadcast_to(atol, d.shape)), (tag, d.tolist())
 
 
 def _rows(results):
@@ -36,8 +41,10 @@ def test_wav_cases_match_reference(golden, gpu):
             continue
         path = os.path.join(DATA, case["wav"])
         got = decode_ft8_from_wave(path, **case["kwargs"])         # int16 path, on-device scaling
-        _same(_rows(got), _gold_rows(case), case["name"])
         x, fs = read_wave_file(path)
+        gold = _gold_rows(case)
+        print(case["name"], "score |diff|", [abs(g[7] - r[7]) for g, r in zip(_rows(got), gold)])
+        _same(_rows(got), gold, case["name"])
         got2 = decode_ft8_message(x, fs, **case["kwargs"])         # float32 path
         assert _rows(got2) == _rows(got), case["name"]
         seen += 1

@@ -106,4 +106,5 @@ def test_gpu_decode_on_reference_test_geometry(reft, gpu, name):
             (r["payload"], r["hash"], r["ldpc_errors"], r["crc_extracted"], r["crc_calculated"], r["time_sec"],
              r["freq_hz"])
         assert type(sc).__name__ == r["score_dtype"]
-        assert abs(float(sc) - r["score"]) <= 2e-3
+        # float64 input: a float64 FFT (1e-9); float32: a float32 FFT's rounding (1e-4)
+        assert abs(float(sc) - r["score"]) <= (1e-9 if r["score_dtype"] == "float64" else 1e-4)

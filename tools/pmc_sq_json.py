@@ -14,6 +14,19 @@ import json
 import sys
 
 
+def build_id():
+    """FT8_BUILD_ID of the library in this tree (the build the counters were collected on: the
+    passes run from the same tree, right before this script); bench.py reports the counters only
+    when it equals the id of the library it loads."""
+    import ctypes
+    import os
+    lib = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "ft8_demodulator_amd", "lib",
+                       "libft8hip.so")
+    L = ctypes.CDLL(lib)
+    L.ft8_build_id.restype = ctypes.c_char_p
+    return L.ft8_build_id().decode()
+
+
 def main():
     last = collections.defaultdict(dict)
     for f in glob.glob(f"{sys.argv[1]}/**/*counter_collection.csv", recursive=True):
@@ -40,7 +53,7 @@ def main():
             v["resident_waves_per_cu"] = 4.0 * wc / 256.0 / g
             v["kernel_cycles"] = g
         out[k] = v
-    json.dump({"source": sys.argv[3] if len(sys.argv) > 3 else sys.argv[1], "kernels": out},
+    json.dump({"build_id": build_id(), "source": sys.argv[3] if len(sys.argv) > 3 else sys.argv[1], "kernels": out},
               open(sys.argv[2], "w"), indent=1)
 
 

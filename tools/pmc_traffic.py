@@ -14,6 +14,19 @@ import json
 import sys
 
 
+def build_id():
+    """FT8_BUILD_ID of the library in this tree (the build the counters were collected on: the
+    passes run from the same tree, right before this script); bench.py reports the counters only
+    when it equals the id of the library it loads."""
+    import ctypes
+    import os
+    lib = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "ft8_demodulator_amd", "lib",
+                       "libft8hip.so")
+    L = ctypes.CDLL(lib)
+    L.ft8_build_id.restype = ctypes.c_char_p
+    return L.ft8_build_id().decode()
+
+
 def per_kernel(d, counter):
     acc = collections.defaultdict(list)
     for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
@@ -35,7 +48,7 @@ def main():
         f, w = fetch.get(k), write.get(k)
         out[k] = {"fetch_bytes_raw": f, "fetch_bytes_x2": 2 * f if f is not None else None, "write_bytes": w,
                   "hbm_bytes": (2 * f if f is not None else 0) + (w or 0)}
-    json.dump({"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE passes of tools/bp_only.py "
+    json.dump({"build_id": build_id(), "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE passes of tools/bp_only.py "
                          "(256 slots, config 3); FETCH_SIZE doubled per the gfx950 correction",
                "kernels": out}, open(sys.argv[3], "w"), indent=1)
     for k, v in out.items():
