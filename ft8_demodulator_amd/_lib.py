@@ -62,6 +62,14 @@ RESULT_DTYPE = np.dtype({
     "itemsize": 40,
 })
 
+# ft8_sub_fit (1056 bytes)
+SUB_FIT_DTYPE = np.dtype({
+    "names": ["active", "start", "f0", "amp", "phase0", "tones"],
+    "formats": ["<i4", "<i8", "<f8", ("<f4", (79, 2)), ("<f4", (80,)), ("u1", (80,))],
+    "offsets": [0, 8, 16, 24, 656, 976],
+    "itemsize": 1056,
+})
+
 # ft8_tx_signal (40 bytes)
 TX_SIGNAL_DTYPE = np.dtype({
     "names": ["f0", "amplitude", "phase", "start", "slot", "reserved"],
@@ -127,6 +135,7 @@ def lib():
             "ft8_set_timing_stages": ([vp, ctypes.c_uint32], ctypes.c_int),
             "ft8_sync_score": ([vp, vp, ctypes.c_int, i32, i32, i32, i32, vp, i32, vp, vp, vp], ctypes.c_int),
             "ft8_pack_bytes": ([i32, i32], i64),
+            "ft8_subtract_fits": ([vp, vp, i32, i32, vp], ctypes.c_int),
             "ft8_pack_decodes": ([vp, vp, vp, i32, i32, i32, i32, vp, vp, vp], ctypes.c_int),
         }
         for name, (args, res) in sig.items():
@@ -171,7 +180,7 @@ EXPORTED_SYMBOLS = (
     "ft8_crc14", "ft8_ldpc_check", "ft8_set_timing", "ft8_get_timing", "ft8_get_counters", "ft8_set_pipeline",
     "ft8_encode", "ft8_synthesize", "ft8_subtract", "ft8_stft_argmax", "ft8_drift_fit", "ft8_drift_correct",
     "ft8_build_id", "ft8_build_flags", "ft8_replay_stage", "ft8_set_timing_stages", "ft8_sync_score",
-    "ft8_pack_bytes", "ft8_pack_decodes")
+    "ft8_pack_bytes", "ft8_pack_decodes", "ft8_subtract_fits")
 
 
 def limits():

@@ -57,6 +57,7 @@ struct ft8_ctx {
   DevBuf wf, scores, smask, cand, cand_score, cand_count, warn, rowsum, res_all, work, stats, llr, tie;
   // FT8_FLAG_SUBTRACT: residual samples, per-record fits, pass-1 / pass-2 records
   DevBuf residual, sub_est, out1, counts1, out2, counts2;
+  int sub_slots = 0, sub_cap = 0;  // shape of the fits in sub_est (ft8_subtract_fits)
   // cumulative GFSK pulse of the transmit chain for one nsps (double and float)
   int gfsk_nsps = 0;
   DevBuf gfsk_P, gfsk_Pf;
@@ -683,6 +684,8 @@ int subtract_core(ft8_ctx* c, const void* x, int dtype, float* resid, int64_t n_
   L.Pf = (const float*)c->gfsk_Pf.p;
   L.est = c->sub_est.p;
   L.Q = Q;
+  c->sub_slots = n_slots;
+  c->sub_cap = cap;
   StageTimer tm(c, 7, s);
   hipError_t e = launch_subtract(L, s);
   tm.done();
@@ -1111,6 +1114,19 @@ int ft8_subtract(ft8_ctx* c, const void* d_samples, int dtype, float* d_residual
   DeviceGuard dg(c->device);
   return subtract_core(c, d_samples, dtype, d_residual, n_samples, n_slots, slot_stride, slot_stride, p, d_res,
                        d_counts, cap, (hipStream_t)stream);
+}
+
+int ft8_subtract_fits(ft8_ctx* c, ft8_sub_fit* d_out, int32_t n_slots, int32_t cap, void* stream) {
+  if (!c || (!d_out && n_slots > 0 && cap > 0)) return fail(c, FT8_E_ARG, "bad argument");
+  if (n_slots != c->sub_slots || cap != c->sub_cap)
+    return fail(c, FT8_E_ARG, "n_slots / cap differ from the last subtraction's (" + std::to_string(c->sub_slots) +
+                                  " / " + std::to_string(c->sub_cap) + ")");
+  if (n_slots == 0 || cap == 0) return FT8_OK;
+  DeviceGuard dg(c->device);
+  static_assert(sizeof(ft8_sub_fit) == 1056, "ft8_sub_fit layout");
+  hipError_t e = hipMemcpyAsync(d_out, c->sub_est.p, sizeof(ft8_sub_fit) * (size_t)n_slots * cap,
+                                hipMemcpyDeviceToDevice, (hipStream_t)stream);
+  return e == hipSuccess ? FT8_OK : hipfail(c, e, "fits copy");
 }
 
 int ft8_stft_argmax(ft8_ctx* c, const void* d_samples, int dtype, int64_t n_samples, int32_t n_slots,

@@ -34,14 +34,9 @@ constexpr int kMaxHyp = 1024;
 constexpr int kMaxT = kMaxQ + 3;                // start offsets searched: 2 ceil(Q / (2 sps)) + 1
 constexpr int kMf = 2;                         // tone-0 search: 2 kMf + 1 points over +-bin/2
 
-struct SubEst {
-  int32_t active, pad;
-  int64_t start;           // refined first sample of the waveform in the slot
-  double f0;               // refined tone-0 frequency, Hz
-  float A[tx::kSymbols][2];
-  float ph0[tx::kSymbols + 1];   // phase (cycles, fractional part) at the start of every symbol
-  uint8_t tones[80];
-};
+// the fitted signal of one record: the public ft8_sub_fit (include/ft8hip.h, ft8_subtract_fits)
+using SubEst = ft8_sub_fit;
+static_assert(sizeof(((SubEst*)nullptr)->amp) / sizeof(float[2]) == tx::kSymbols, "one amplitude per symbol");
 
 template <typename InT>
 __device__ __forceinline__ float ld_sample(const InT* x, int64_t i);
@@ -321,10 +316,10 @@ __global__ __launch_bounds__(kSubThreads) void k_sub_est(SubLaunch a) {
     else
       v = make_float2(0.25f * (s_A[k - 1].x + 2.f * s_A[k].x + s_A[k + 1].x),
                       0.25f * (s_A[k - 1].y + 2.f * s_A[k].y + s_A[k + 1].y));
-    est->A[k][0] = v.x;
-    est->A[k][1] = v.y;
+    est->amp[k][0] = v.x;
+    est->amp[k][1] = v.y;
   }
-  if (threadIdx.x <= tx::kSymbols) est->ph0[threadIdx.x] = s_ph0[threadIdx.x];
+  if (threadIdx.x <= tx::kSymbols) est->phase0[threadIdx.x] = s_ph0[threadIdx.x];
   if (threadIdx.x < 80) est->tones[threadIdx.x] = threadIdx.x < tx::kSymbols ? s_tones[threadIdx.x] : 0;
   if (threadIdx.x == 0) {
     est->start = start;
@@ -366,8 +361,8 @@ __global__ __launch_bounds__(kSubThreads) void k_sub_apply(SubLaunch a) {
       const int jj = (int)threadIdx.x - 1;
       s_E[threadIdx.x] = e->tones[jj < 0 ? 0 : (jj > tx::kSymbols - 1 ? tx::kSymbols - 1 : jj)];
     }
-    if (threadIdx.x < tx::kSymbols) s_A[threadIdx.x] = make_float2(e->A[threadIdx.x][0], e->A[threadIdx.x][1]);
-    if (threadIdx.x <= tx::kSymbols) s_ph0[threadIdx.x] = e->ph0[threadIdx.x];
+    if (threadIdx.x < tx::kSymbols) s_A[threadIdx.x] = make_float2(e->amp[threadIdx.x][0], e->amp[threadIdx.x][1]);
+    if (threadIdx.x <= tx::kSymbols) s_ph0[threadIdx.x] = e->phase0[threadIdx.x];
     __syncthreads();
     const float f0r = (float)(e->f0 / (double)a.fs), sr = 6.25f / fsf;
 #pragma unroll

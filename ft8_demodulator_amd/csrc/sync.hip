@@ -175,15 +175,18 @@ __global__ void k_score_list(const T* wf, int Tn, int F, int sps, int bpt, const
 // ---- k_score2 ----------------------------------------------------------------------------------
 constexpr int kS2TW = 128;                 // grid columns per workgroup (64 lanes x 2)
 constexpr int kS2R = 22;                   // grid rows per workgroup (88 = 4 x 22 at 12 kHz)
-constexpr int kS2Waves = 11;               // each wave takes rows w, w + 11
+constexpr int kS2Waves = 8;                // row j of the workgroup on wave j % 8
+constexpr int kS2Rows = (kS2R + kS2Waves - 1) / kS2Waves;  // rows per wave (3, the last two waves 2)
 constexpr int kS2Threads = kS2Waves * kWave;
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 template <int BPT, int SPS>
 struct S2Geom {
   static constexpr int P = (kS2TW + 7 * BPT + 3) & ~3;   // staged columns (multiple of 4: float4 rows)
-  static constexpr int H = kS2R + 8 * SPS;               // staged rows per Costas band
-  static constexpr int kFloats = 3 * H * P;
+  static constexpr int H = kS2R + 8 * SPS;               // staged rows of one Costas band
+  static constexpr int kFloats = H * P;                  // the LDS tile: one band at a time
+  static constexpr int Q = P / 4;                        // float4 per staged row
+  static constexpr int kIter = (H * Q + kS2Threads - 1) / kS2Threads;  // float4 staged per thread
 };
 
 // maximum over the wave (no NaN), on order-preserving integer keys (a float max would re-quiet
@@ -217,14 +220,38 @@ __device__ __forceinline__ f32x2 ld2(const float* p) {
   else return f32x2{p[0], p[1]};
 }
 
+// Costas band m of the tile (staged rows [a0 - SPS + 36 m SPS, + H), columns [c0, c0 + P)) as float4
+// loads into registers; rows outside the waterfall / columns past F are zero and never read by a
+// valid candidate.  Thread t owns float4 t + 512 it.
+template <int BPT, int SPS>
+__device__ __forceinline__ void s2_load(const float* wf, int T, int F, int a0, int c0, int m,
+                                        float4 (&v)[S2Geom<BPT, SPS>::kIter]) {
+  using G = S2Geom<BPT, SPS>;
+#pragma unroll
+  for (int it = 0; it < G::kIter; ++it) {
+    const int idx = (int)threadIdx.x + it * kS2Threads;
+    const int rw = idx / G::Q, q4 = idx - rw * G::Q;
+    const int row = a0 - SPS + 36 * m * SPS + rw, col = c0 + 4 * q4;
+    v[it] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (idx < G::H * G::Q && row >= 0 && row < T && col < F)
+      v[it] = *reinterpret_cast<const float4*>(wf + (int64_t)row * F + col);
+  }
+}
+
+// One workgroup: 128 grid columns x 22 grid rows of one slot.  The three Costas bands of the
+// waterfall the candidates read are staged into LDS ONE AT A TIME (22 KB at bpt = sps = 2, so four
+// workgroups -- 32 waves -- share a CU), band m + 1's global loads in flight while band m is scored;
+// each wave keeps its rows' two-column partial sums in registers across the bands, so every score
+// still accumulates its 75 terms in the reference's order (band, symbol, tone-1, tone+1, time-1,
+// time+1).
 template <int BPT, int SPS, bool COMPACT>
 __global__ __launch_bounds__(kS2Threads) void k_score2(ScoreArgs a) {
   static_assert(kS2TW == kSegCols, "a workgroup's columns are one score segment");
   using G = S2Geom<BPT, SPS>;
-  constexpr int P = G::P, H = G::H;
+  constexpr int P = G::P;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float* tile = reinterpret_cast<float*>(smem);
-  // workgroup -> (slot, band, column tile); slot % 8 == workgroup id % 8 keeps a slot on one XCD
+  // workgroup -> (slot, row tile, column tile); slot % 8 == workgroup id % 8 keeps a slot on one XCD
   const int id = blockIdx.x;
   const int per = a.n_bands * a.n_ctiles;
   const int q = id >> 3;
@@ -235,76 +262,63 @@ __global__ __launch_bounds__(kS2Threads) void k_score2(ScoreArgs a) {
   const int a0 = a.t0 + band * kS2R;
   const int c0 = ct * kS2TW;
   const float* wf = reinterpret_cast<const float*>(a.wf) + (int64_t)slot * a.T * a.F;
-
-  // stage band m: waterfall rows [a0 + 36 m SPS - SPS, + H), columns [c0, c0 + P).  Rows are
-  // P / 4 float4s; every thread issues all its loads before its first LDS store, so the staging
-  // costs one memory round trip (rows outside the waterfall / columns past F are zero and never
-  // read by a valid candidate)
-  if ((a.F & 3) == 0) {
-    // thread -> (float4 column q4, staged row r0 + RPI it): the index math is done once, each
-    // further row is a compile-time step
-    constexpr int Q = P / 4, RPI = kS2Threads / Q, NR = 3 * H;
-    constexpr int kIter = (NR + RPI - 1) / RPI;
-    const int q4 = (int)threadIdx.x % Q, r0 = (int)threadIdx.x / Q;
-    const int col = c0 + 4 * q4;
-    const bool cok = r0 < RPI && col < a.F;
-    const float* wc = wf + col;
-    float4 v[kIter];
-#pragma unroll
-    for (int it = 0; it < kIter; ++it) {
-      const int rw = r0 + it * RPI;   // staged row: band m = rw / H (two compares), row in band
-      const int m = (rw >= H ? 1 : 0) + (rw >= 2 * H ? 1 : 0);
-      const int row = a0 - SPS + rw + m * (36 * SPS - H);
-      v[it] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (cok && rw < NR && row >= 0 && row < a.T) v[it] = *reinterpret_cast<const float4*>(wc + row * a.F);
-    }
-#pragma unroll
-    for (int it = 0; it < kIter; ++it) {
-      const int rw = r0 + it * RPI;
-      if (r0 < RPI && rw < NR) reinterpret_cast<float4*>(tile)[rw * Q + q4] = v[it];
-    }
-  } else {
-    for (int i = threadIdx.x; i < G::kFloats; i += kS2Threads) {
-      const int m = i / (H * P), rem = i - m * (H * P);
-      const int rr = rem / P, cc = rem - rr * P;
-      const int row = a0 + 36 * m * SPS - SPS + rr, col = c0 + cc;
-      float v = 0.0f;
-      if (row >= 0 && row < a.T && col < a.F) v = wf[(int64_t)row * a.F + col];
-      tile[i] = v;
-    }
-  }
-  __syncthreads();
+  const bool vec = (a.F & 3) == 0;
 
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const int af = c0 + 2 * lane;
   const int nb = a.num_blocks;
   const int rows = min(kS2R, a.t0 + a.NT - a0);
-  float* out = reinterpret_cast<float*>(a.scores) + (COMPACT ? 0 : (int64_t)slot * a.NT * a.NF);
-  RowSummary* rs = a.rowsum + (int64_t)slot * a.NT;
-  for (int j = w; j < rows; j += kS2Waves) {
-    const int at = a0 + j;                 // wave-uniform
-    const int base = floordiv(at, SPS);
-    f32x2 score = {0.0f, 0.0f};
-    int n = 0;
-    const float* tb = tile + j * P + 2 * lane;
+  f32x2 score[kS2Rows];
+  int n[kS2Rows];
 #pragma unroll
-    for (int m = 0; m < 3; ++m) {
-      const int lo = base + 36 * m;  // block index of the band's first Costas symbol
+  for (int u = 0; u < kS2Rows; ++u) {
+    score[u] = f32x2{0.0f, 0.0f};
+    n[u] = 0;
+  }
+
+  float4 v[G::kIter];
+  if (vec) s2_load<BPT, SPS>(wf, a.T, a.F, a0, c0, 0, v);
+#pragma unroll 1
+  for (int m = 0; m < 3; ++m) {
+    if (m > 0) __syncthreads();  // every wave has scored band m - 1
+    if (vec) {
+#pragma unroll
+      for (int it = 0; it < G::kIter; ++it) {
+        const int idx = (int)threadIdx.x + it * kS2Threads;
+        if (idx < G::H * G::Q) reinterpret_cast<float4*>(tile)[idx] = v[it];
+      }
+      if (m < 2) s2_load<BPT, SPS>(wf, a.T, a.F, a0, c0, m + 1, v);  // in flight while band m is scored
+    } else {
+      for (int i = threadIdx.x; i < G::kFloats; i += kS2Threads) {
+        const int rr = i / P, cc = i - rr * P;
+        const int row = a0 + 36 * m * SPS - SPS + rr, col = c0 + cc;
+        float x = 0.0f;
+        if (row >= 0 && row < a.T && col < a.F) x = wf[(int64_t)row * a.F + col];
+        tile[i] = x;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < kS2Rows; ++u) {
+      const int j = w + u * kS2Waves;        // wave-uniform
+      if (j >= rows) continue;
+      const int lo = floordiv(a0 + j, SPS) + 36 * m;  // block index of the band's first Costas symbol
+      const float* tb = tile + j * P + 2 * lane;
       if (lo >= 0 && lo <= nb - 7) {
-        // every symbol of the band and all its neighbours in range: straight-line code, so the
-        // 35 loads issue together (25 differences, in the reference order)
+        // every symbol of the band and all its neighbours in range: straight-line code
+        // (25 differences, in the reference order)
 #pragma unroll
         for (int k = 0; k < 7; ++k) {
           const int tone = kCostasC[k];
-          const float* rp = tb + (m * H + (k + 1) * SPS) * P + tone * BPT;
+          const float* rp = tb + (k + 1) * SPS * P + tone * BPT;
           const f32x2 pw = ld2<BPT>(rp);
-          if (tone > 0) score += pw - ld2<BPT>(rp - BPT);
-          if (tone < 7) score += pw - ld2<BPT>(rp + BPT);
-          if (k > 0) score += pw - ld2<BPT>(rp - SPS * P);
-          if (k < 6) score += pw - ld2<BPT>(rp + SPS * P);
+          if (tone > 0) score[u] += pw - ld2<BPT>(rp - BPT);
+          if (tone < 7) score[u] += pw - ld2<BPT>(rp + BPT);
+          if (k > 0) score[u] += pw - ld2<BPT>(rp - SPS * P);
+          if (k < 6) score[u] += pw - ld2<BPT>(rp + SPS * P);
         }
-        n += 25;
+        n[u] += 25;
       } else if (lo + 6 >= 0 && lo < nb) {
         // a band crossing the waterfall's first or last block: the reference's per-term tests
 #pragma unroll
@@ -312,22 +326,30 @@ __global__ __launch_bounds__(kS2Threads) void k_score2(ScoreArgs a) {
           const int ba = lo + k;
           if (ba < 0 || ba >= nb) continue;
           const int tone = kCostasC[k];
-          const float* rp = tb + (m * H + (k + 1) * SPS) * P + tone * BPT;
+          const float* rp = tb + (k + 1) * SPS * P + tone * BPT;
           const f32x2 pw = ld2<BPT>(rp);
-          if (tone > 0) { score += pw - ld2<BPT>(rp - BPT); n++; }
-          if (tone < 7) { score += pw - ld2<BPT>(rp + BPT); n++; }
-          if (k > 0 && ba > 0) { score += pw - ld2<BPT>(rp - SPS * P); n++; }
-          if (k < 6 && ba + 1 < nb) { score += pw - ld2<BPT>(rp + SPS * P); n++; }
+          if (tone > 0) { score[u] += pw - ld2<BPT>(rp - BPT); n[u]++; }
+          if (tone < 7) { score[u] += pw - ld2<BPT>(rp + BPT); n[u]++; }
+          if (k > 0 && ba > 0) { score[u] += pw - ld2<BPT>(rp - SPS * P); n[u]++; }
+          if (k < 6 && ba + 1 < nb) { score[u] += pw - ld2<BPT>(rp + SPS * P); n[u]++; }
         }
       }
     }
+  }
+
+  float* out = reinterpret_cast<float*>(a.scores) + (COMPACT ? 0 : (int64_t)slot * a.NT * a.NF);
+  RowSummary* rs = a.rowsum + (int64_t)slot * a.NT;
+#pragma unroll
+  for (int u = 0; u < kS2Rows; ++u) {
+    const int j = w + u * kS2Waves;
+    if (j >= rows) continue;
     float res[2];
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
-      const float sc = score[c];
-      res[c] = (n == 0 || isnan(sc) || isinf(sc)) ? -INFINITY : sc / (float)n;
+      const float sc = score[u][c];
+      res[c] = (n[u] == 0 || isnan(sc) || isinf(sc)) ? -INFINITY : sc / (float)n[u];
     }
-    const int ti = at - a.t0;
+    const int ti = a0 + j - a.t0;
     const bool v0 = af < a.NF, v1 = af + 1 < a.NF;
     const bool p0 = v0 && passes(res[0], a.min_score, a.cmp_f64);
     const bool p1 = v1 && passes(res[1], a.min_score, a.cmp_f64);
@@ -367,13 +389,7 @@ hipError_t launch_score2(const SyncLaunch& L, const ScoreArgs& a0, hipStream_t s
   a.n_bands = (L.NT + kS2R - 1) / kS2R;
   a.n_ctiles = (L.NF + kS2TW - 1) / kS2TW;
   const size_t lds = sizeof(float) * G::kFloats;
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_score2<BPT, SPS, COMPACT>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
-    attr = true;
-  }
+  static_assert(sizeof(float) * S2Geom<4, 4>::kFloats <= 64 * 1024, "one band fits the default LDS limit");
   const int groups = (L.n_slots + 7) / 8;
   const int64_t blocks = (int64_t)groups * 8 * a.n_bands * a.n_ctiles;
   hipLaunchKernelGGL((k_score2<BPT, SPS, COMPACT>), dim3((unsigned)blocks), dim3(kS2Threads), lds, s, a);

@@ -250,6 +250,22 @@ int ft8_subtract(ft8_ctx* ctx, const void* d_samples, int dtype, float* d_residu
                  int32_t n_slots, int64_t slot_stride, const ft8_params* p, const ft8_result* d_res,
                  const int32_t* d_counts, int32_t cap, void* stream);
 
+/* The signals the last subtraction of this context fitted (ft8_subtract, or pass 1 of an
+ * FT8_FLAG_SUBTRACT ft8_decode_batch, whose cap is max_candidates): fit of record r of slot s at
+ * d_out[s * cap + r] for r < min(counts[s], cap), copied device -> device.  n_slots and cap must
+ * equal that subtraction's.  The residual is x - sum over the active fits of
+ * ramp(n) Re(A(n) exp(2 pi i phase(n))), A interpolated linearly between symbol centres. */
+typedef struct ft8_sub_fit {
+  int32_t active;          /* 1: fitted and subtracted; 0: failed record, or a payload an earlier record carries */
+  int32_t reserved;
+  int64_t start;           /* refined first sample of the 79-symbol waveform (slot sample index) */
+  double f0;               /* refined tone-0 frequency, Hz */
+  float amp[79][2];        /* complex amplitude per symbol ([1 2 1]-smoothed), (re, im) */
+  float phase0[80];        /* carrier phase in cycles (fractional part) at the start of each symbol */
+  uint8_t tones[80];       /* the payload's re-encoded tone sequence (79 used) */
+} ft8_sub_fit;
+int ft8_subtract_fits(ft8_ctx* ctx, ft8_sub_fit* d_out, int32_t n_slots, int32_t cap, void* stream);
+
 /* ---- frequency-drift correction (ft8_beacon_receiver/frequency_correction.py) -------------
  * Paths below are relative to src/ft8_tools/ft8_beacon_receiver/.  Parameters of
  * correct_frequency_drift (frequency_correction.py:118-163); fields default to the reference's

@@ -240,23 +240,29 @@ def test_decode_batch_orders_equal_scores_like_the_reference(gpu, oracle):
 
 
 @pytest.mark.gpu
-def test_compacted_records_on_device(gpu):
-    """distributed.compact_records (the N > 1 gather's packing) on real decode output: the dense rows
-    are every slot's decodes in slot order, identical to SlotDecoder.records()."""
+def test_packed_records_on_device(gpu):
+    """ft8_pack_decodes (the N > 1 exchange's device packing) on real decode output: the packed rows
+    are every slot's decodes in slot order, identical to SlotDecoder.records(); with a capacity
+    below the total, the rest lands in the overflow rows in order."""
     import numpy as np
     import torch
     from ft8_demodulator_amd import SlotDecoder, _lib, synth
-    from ft8_demodulator_amd.distributed import compact_records
+    from ft8_demodulator_amd.distributed import header_bytes, pack_decodes
     x, _ = synth.make_slots(12, 30, seed=321, device="cuda")
     dec = SlotDecoder(12000, 2, 2, 300, 2, 20)
     out, counts = dec.run(x)
-    dense, total = compact_records(out, counts, dec.cap, 64)
+    send, _ = pack_decodes(out, counts, dec.cap, 64)
     torch.cuda.synchronize()
     per_slot = dec.records(x)
     want = np.concatenate([r for r in per_slot]) if per_slot else np.zeros(0, _lib.RESULT_DTYPE)
-    assert int(total) == len(want) >= 3
-    got = dense[: int(total)].cpu().numpy().reshape(-1).view(_lib.RESULT_DTYPE)
+    h = header_bytes(12)
+    total = int(send[:8].cpu().view(torch.int64))
+    assert total == len(want) >= 3
+    assert send[8:8 + 48].cpu().view(torch.int32).tolist() == counts.cpu().tolist()
+    got = send[h:h + 40 * total].cpu().numpy().view(_lib.RESULT_DTYPE)
     assert got.tobytes() == want.tobytes()
-    small, total2 = compact_records(out, counts, dec.cap, 3)
-    assert int(total2) == len(want) and small.shape[0] == 3
-    assert small.cpu().numpy().reshape(-1).view(_lib.RESULT_DTYPE).tobytes() == want[:3].tobytes()
+    small, over = pack_decodes(out, counts, dec.cap, 3)
+    rows = small[h:].cpu().numpy().view(_lib.RESULT_DTYPE)
+    assert int(small[:8].cpu().view(torch.int64)) == len(want) and len(rows) == 3
+    assert rows.tobytes() == want[:3].tobytes()
+    assert over[: total - 3].cpu().numpy().tobytes() == want[3:].tobytes()
