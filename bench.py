@@ -273,6 +273,64 @@ def drift_cpu_baseline(procs, n=32):
             "wall_s": dt}
 
 
+def drift_32k(dev, n_sig=16, reps=3):
+    """The reference drift test's own rate (test_correction.py:93): 32 768 Hz complex128 beacons,
+    nfft 10 485 = 3^2 5 233 -- an FFT length the Stockham plans cannot take, so both STFT-argmax
+    passes run the chirp-z transform (ft8_stft_method).  Per-signal time of ft8_drift_correct."""
+    import ctypes
+    import numpy as np
+    import torch
+    from ft8_demodulator_amd import _lib, ft8_generator as G
+    from ft8_demodulator_amd.frequency_correction import _drift_params, DEFAULT_PARAMS
+    fs = 32768
+    nsps = int(0.16 * fs)
+    L = 79 * nsps
+    n = 3 * L
+    prm = drift_signal_params(n_sig, seed=32768)
+    pays = np.frombuffer(b"".join(bytes.fromhex(p[0]) for p in prm), dtype=np.uint8).reshape(-1, 10)
+    _, _, tones = G.encode_batch(pays, device=dev)
+    sig = np.array([(p[1] + p[2], 1.0, 0.0, L, i, 0) for i, p in enumerate(prm)], dtype=_lib.TX_SIGNAL_DTYPE)
+    x = G.synthesize(tones, sig, n_sig, n, fs, _lib.FT8_TX_REFERENCE, dtype=torch.complex128, device=dev)
+    t = torch.arange(n, device=dev, dtype=torch.float64)
+    k = torch.tensor([p[3] for p in prm], device=dev, dtype=torch.float64)[:, None] / fs
+    x *= torch.polar(torch.ones((), device=dev, dtype=torch.float64), 2 * np.pi * k * t * t / (2 * fs))
+    g = torch.Generator(device=dev)
+    g.manual_seed(8)
+    sd = torch.sqrt((x.abs() ** 2).mean(dim=1, keepdim=True) / 10 ** 2.8 * fs / 2)
+    x += torch.complex(torch.randn(x.shape, generator=g, device=dev, dtype=torch.float64),
+                       torch.randn(x.shape, generator=g, device=dev, dtype=torch.float64)) * sd
+    del t
+    ctx = _lib.context(dev)
+    out = torch.empty_like(x)
+    res = torch.zeros(n_sig * _lib.DRIFT_RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+    p = _drift_params(dict(DEFAULT_PARAMS, **DRIFT_PARAMS), fs, 6.25, 0.16)
+    st = _lib.stream_handle(dev)
+    method = _lib.lib().ft8_stft_method(ctx.handle, fs, DRIFT_PARAMS["bins_per_tone"], DRIFT_PARAMS["steps_per_symbol"],
+                                        n, _lib.FT8_C128)
+
+    def run():
+        ctx.check(_lib.lib().ft8_drift_correct(ctx.handle, _lib.ptr(x), _lib.FT8_C128, n, n_sig, n, ctypes.byref(p),
+                                               _lib.ptr(out), _lib.ptr(res), st), "ft8_drift_correct")
+
+    run()
+    torch.cuda.synchronize()
+    r = res.cpu().numpy().view(_lib.DRIFT_RESULT_DTYPE)
+    ok = r["status"] == _lib.FT8_DRIFT_FULL
+    est = np.asarray(r["rate_per_sample"]) * fs
+    true = np.array([p_[3] for p_ in prm])
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        run()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / reps
+    del x, out
+    return {"workload": f"correct_frequency_drift on {n_sig} complex128 beacons at 32768 Hz x {n} samples "
+                        "(the reference drift test's rate: nfft 10485 = 3^2 5 233)",
+            "stft_method": {0: "stockham", 1: "packed3840", 2: "chirp-z", 3: "direct DFT"}.get(method, method),
+            "ms_per_signal": dt / n_sig * 1e3, "signals_per_s": n_sig / dt, "full_fits": int(ok.sum()),
+            "median_abs_rate_err_hz_per_s": float(np.median(np.abs(est[ok] - true[ok]))) if ok.any() else None}
+
+
 def drift_correct(dev, n_sig=256, reps=5):
     """The beacon receiver's correct_frequency_drift (frequency_correction.py:118-659) on a batch of
     n_sig independent complex128 beacons: 12 kHz, the reference test's layout (12.64 s of signal
@@ -691,6 +749,7 @@ def main():
     if world == 1 and not args.no_drift:
         drift = drift_correct(dev)
         drift["cpu_baseline"] = drift_cpu_port
+        drift["rate_32768"] = drift_32k(dev)
     sub = None
     if world == 1 and not args.no_subtract:
         sub = subtract_redecode(dev)

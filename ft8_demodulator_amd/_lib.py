@@ -18,6 +18,7 @@ FT8_F32, FT8_F64, FT8_C64, FT8_C128, FT8_I16 = 0, 1, 2, 3, 4
 FT8_OK, FT8_E_ARG, FT8_E_HIP, FT8_E_UNSUPPORTED, FT8_E_NOMEM, FT8_E_RANGE = 0, -1, -2, -3, -4, -5
 FT8_FLAG_TOPK, FT8_FLAG_SUBTRACT = 1, 2
 FT8_TX_PROTOCOL, FT8_TX_REFERENCE = 0, 1
+FT8_STFT_STOCKHAM, FT8_STFT_PACKED3840, FT8_STFT_CHIRPZ, FT8_STFT_DFT = 0, 1, 2, 3
 N_STAGES = 11
 STAGE_NAMES = ("stft", "score", "select", "bp", "compact", "decode_batch", "llr", "subtract",
                "drift_stft_argmax", "drift_fit", "drift_derotate")
@@ -136,6 +137,7 @@ def lib():
             "ft8_sync_score": ([vp, vp, ctypes.c_int, i32, i32, i32, i32, vp, i32, vp, vp, vp], ctypes.c_int),
             "ft8_pack_bytes": ([i32, i32], i64),
             "ft8_subtract_fits": ([vp, vp, i32, i32, vp], ctypes.c_int),
+            "ft8_stft_method": ([vp, i32, i32, i32, i64, ctypes.c_int], ctypes.c_int),
             "ft8_pack_decodes": ([vp, vp, vp, i32, i32, i32, i32, vp, vp, vp], ctypes.c_int),
         }
         for name, (args, res) in sig.items():
@@ -180,7 +182,7 @@ EXPORTED_SYMBOLS = (
     "ft8_crc14", "ft8_ldpc_check", "ft8_set_timing", "ft8_get_timing", "ft8_get_counters", "ft8_set_pipeline",
     "ft8_encode", "ft8_synthesize", "ft8_subtract", "ft8_stft_argmax", "ft8_drift_fit", "ft8_drift_correct",
     "ft8_build_id", "ft8_build_flags", "ft8_replay_stage", "ft8_set_timing_stages", "ft8_sync_score",
-    "ft8_pack_bytes", "ft8_pack_decodes", "ft8_subtract_fits")
+    "ft8_pack_bytes", "ft8_pack_decodes", "ft8_subtract_fits", "ft8_stft_method")
 
 
 def limits():

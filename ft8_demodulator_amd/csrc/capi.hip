@@ -30,9 +30,12 @@ struct PlanEntry {
   int nfft;
   bool cplx;   // complex-input path (P = nfft) vs real-input half-length path (P = nfft/2)
   bool f64;
+  int L = 0;   // nperseg (chirp-z plans are built for one)
   FftPlan plan;
   void* tw = nullptr;
   void* post = nullptr;
+  void* chirp = nullptr;
+  void* hspec = nullptr;
 };
 
 struct WinEntry {
@@ -280,23 +283,122 @@ bool factor(int P, FftPlan& pl) {
   return r == 1 && pl.nstages > 0;
 }
 
-int get_plan(ft8_ctx* c, int nfft, bool cplx, bool f64, FftPlan* out) {
+// in-place radix-2 FFT (long double, host) of a power-of-two length: the chirp-z filter spectra
+void host_fft_pow2(std::vector<long double>& re, std::vector<long double>& im) {
+  const size_t n = re.size();
+  for (size_t i = 1, j = 0; i < n; ++i) {
+    size_t bit = n >> 1;
+    for (; j & bit; bit >>= 1) j ^= bit;
+    j ^= bit;
+    if (i < j) {
+      std::swap(re[i], re[j]);
+      std::swap(im[i], im[j]);
+    }
+  }
+  for (size_t len = 2; len <= n; len <<= 1) {
+    for (size_t k = 0; k < len / 2; ++k) {
+      const long double ang = -2.0L * M_PIl * (long double)k / (long double)len;
+      const long double wr = cosl(ang), wi = sinl(ang);
+      for (size_t i = k; i < n; i += len) {
+        const size_t j = i + len / 2;
+        const long double xr = re[j] * wr - im[j] * wi, xi = re[j] * wi + im[j] * wr;
+        re[j] = re[i] - xr;
+        im[j] = im[i] - xi;
+        re[i] += xr;
+        im[i] += xi;
+      }
+    }
+  }
+}
+
+// exp(-i pi j^2 / N) from the exact residue j^2 mod 2N
+void chirp_of(int64_t j, int N, long double* cr, long double* ci) {
+  const int64_t r = (j * j) % (2 * (int64_t)N);
+  const long double ang = -M_PIl * (long double)r / (long double)N;
+  *cr = cosl(ang);
+  *ci = sinl(ang);
+}
+
+// the chirp-z tables of a plan (P = the convolution length, a power of two): chirp c(k), k < nfft,
+// and the spectra of the nblk block filters h_b[m] = conj(c(b B + m - (L - 1))), m < P
+int blue_tables(ft8_ctx* c, PlanEntry& e, int nfft, int L, int P, bool f64) {
+  const int B = P - L + 1;
+  const int nblk = (nfft + B - 1) / B;
+  const size_t esz = f64 ? 16 : 8;
+  std::vector<unsigned char> ch(esz * nfft), hs(esz * (size_t)nblk * P);
+  auto put = [&](std::vector<unsigned char>& v, size_t i, long double xr, long double xi) {
+    if (f64) { double t[2] = {(double)xr, (double)xi}; memcpy(&v[esz * i], t, 16); }
+    else { float t[2] = {(float)xr, (float)xi}; memcpy(&v[esz * i], t, 8); }
+  };
+  for (int k = 0; k < nfft; ++k) {
+    long double cr, ci;
+    chirp_of(k, nfft, &cr, &ci);
+    put(ch, k, cr, ci);
+  }
+  std::vector<long double> re(P), im(P);
+  for (int b = 0; b < nblk; ++b) {
+    for (int m = 0; m < P; ++m) {
+      long double cr, ci;
+      chirp_of((int64_t)b * B + m - (L - 1), nfft, &cr, &ci);
+      re[m] = cr;
+      im[m] = -ci;
+    }
+    host_fft_pow2(re, im);
+    for (int m = 0; m < P; ++m) put(hs, (size_t)b * P + m, re[m], im[m]);
+  }
+  hipError_t he = hipMalloc(&e.chirp, ch.size());
+  if (he == hipSuccess) he = hipMalloc(&e.hspec, hs.size());
+  if (he == hipSuccess) he = hipMemcpy(e.chirp, ch.data(), ch.size(), hipMemcpyHostToDevice);
+  if (he == hipSuccess) he = hipMemcpy(e.hspec, hs.data(), hs.size(), hipMemcpyHostToDevice);
+  if (he != hipSuccess) return hipfail(c, he, "chirp-z plan upload");
+  e.plan.L = L;
+  e.plan.B = B;
+  e.plan.nblk = nblk;
+  e.plan.chirp = e.chirp;
+  e.plan.hspec = e.hspec;
+  return FT8_OK;
+}
+
+int get_plan(ft8_ctx* c, int nfft, bool cplx, bool f64, int nperseg, FftPlan* out) {
   for (auto& p : c->plans)
-    if (p.nfft == nfft && p.cplx == cplx && p.f64 == f64) { *out = p.plan; return FT8_OK; }
+    if (p.nfft == nfft && p.cplx == cplx && p.f64 == f64 && (!p.plan.blue || p.L == nperseg)) {
+      *out = p.plan;
+      return FT8_OK;
+    }
   PlanEntry e;
   e.nfft = nfft;
   e.cplx = cplx;
   e.f64 = f64;
   int P = cplx ? nfft : nfft / 2;
   e.plan.dft = 0;
+  e.plan.blue = 0;
   // lengths the LDS Stockham FFT cannot take (a prime factor above 7, odd real nfft, above the
-  // compiled limit) fall back to the direct DFT kernel: P = nfft, tw = W_nfft^m
+  // compiled limit) take the chirp-z transform when its convolution fits the LDS FFT and is the
+  // cheaper one, else the direct DFT kernel (P = nfft, tw = W_nfft^m)
   const int max_p = f64 ? kMaxFftP64 : (cplx ? kMaxFftComplex : kMaxFftReal / 2);
   if ((!cplx && (nfft % 2)) || P > max_p || !factor(P, e.plan)) {
     if (nfft > kMaxDft) return fail(c, FT8_E_RANGE, "nfft " + std::to_string(nfft) + " exceeds the compiled DFT limit");
-    P = nfft;
-    e.plan.dft = 1;
-    e.plan.nstages = 0;
+    // chirp-z: P a power of two >= L + (bins needed) - 1, capped at the LDS FFT limit; cost per frame
+    // ~ blocks x 2 x 5 P log2 P against the direct DFT's 8 L per kept bin
+    const int need = cplx ? nfft : (nfft + 1) / 2;
+    const int pmax = f64 ? kMaxBlueP64 : kMaxBlueP32;
+    int M = 1;
+    while (M < nperseg + need - 1 && M < pmax) M <<= 1;
+    int lg = 0;
+    while ((1 << lg) < M) ++lg;
+    const double blocks = M > nperseg ? std::ceil((double)need / (double)(M - nperseg + 1)) : 0.0;
+    const bool blue = M > nperseg && blocks * 10.0 * M * lg < 8.0 * nperseg * need;
+    if (blue && factor(M, e.plan)) {
+      P = M;
+      e.plan.blue = 1;
+      e.L = nperseg;
+      int rc = blue_tables(c, e, nfft, nperseg, M, f64);
+      if (rc) return rc;
+    } else {
+      P = nfft;
+      e.plan.dft = 1;
+      e.plan.nstages = 0;
+    }
   }
   e.plan.P = P;
   // twiddles W_P^m and post-processing W_N^k (N = 2P), from long double angles
@@ -360,7 +462,7 @@ int do_stft(ft8_ctx* c, const void* samples, int dtype, int64_t n_samples, int n
   if (p->t_hi == p->t_lo || p->f_hi == p->f_lo || n_slots == 0) return FT8_OK;
   const bool f64 = is_f64_dtype(dtype), cplx = is_cplx_dtype(dtype);
   StftLaunch L{};
-  rc = get_plan(c, g.nfft, cplx, f64, &L.plan);
+  rc = get_plan(c, g.nfft, cplx, f64, g.nperseg, &L.plan);
   if (rc) return rc;
   if (L.plan.dft && (size_t)g.nperseg * (f64 ? 16 : 8) > (size_t)kMaxDftLds)
     return fail(c, FT8_E_RANGE, "nperseg " + std::to_string(g.nperseg) + " exceeds the direct-DFT limit");
@@ -709,10 +811,11 @@ int stft_argmax_core(ft8_ctx* c, const void* x, int dtype, int64_t n_samples, in
   if (p->t_hi == p->t_lo || n_slots == 0) return FT8_OK;
   const bool f64 = is_f64_dtype(dtype), cplx = is_cplx_dtype(dtype);
   StftLaunch L{};
-  if ((rc = get_plan(c, g.nfft, cplx, f64, &L.plan))) return rc;
-  if (L.plan.dft) {
-    // the direct DFT writes the dB rows, then reduces each to its argmax: stage them in wf
-    if ((size_t)g.nperseg * (f64 ? 16 : 8) > (size_t)kMaxDftLds)
+  if ((rc = get_plan(c, g.nfft, cplx, f64, g.nperseg, &L.plan))) return rc;
+  if (L.plan.dft || L.plan.blue) {
+    // the direct DFT and the chirp-z path write the dB rows, then reduce each to its argmax: stage
+    // them in wf
+    if (L.plan.dft && (size_t)g.nperseg * (f64 ? 16 : 8) > (size_t)kMaxDftLds)
       return fail(c, FT8_E_RANGE, "nperseg " + std::to_string(g.nperseg) + " exceeds the direct-DFT limit");
     const size_t bytes = (size_t)n_slots * (p->t_hi - p->t_lo) * (p->f_hi - p->f_lo) * (f64 ? 8 : 4);
     if ((rc = ensure(c, c->wf, bytes))) return rc;
@@ -861,6 +964,8 @@ int ft8_destroy(ft8_ctx* c) {
     for (auto& p : c->plans) {
       if (p.tw) (void)hipFree(p.tw);
       if (p.post) (void)hipFree(p.post);
+      if (p.chirp) (void)hipFree(p.chirp);
+      if (p.hspec) (void)hipFree(p.hspec);
     }
     for (auto& w : c->wins)
       if (w.w) (void)hipFree(w.w);
@@ -898,6 +1003,26 @@ int ft8_stft(ft8_ctx* c, const void* d_samples, int dtype, int64_t n_samples, in
   if (!c || !p || (!d_samples && n_slots > 0) || (!d_wf && n_slots > 0)) return fail(c, FT8_E_ARG, "null argument");
   DeviceGuard dg(c->device);
   return do_stft(c, d_samples, dtype, n_samples, n_slots, slot_stride, p, d_wf, (hipStream_t)stream);
+}
+
+int ft8_stft_method(ft8_ctx* c, int32_t fs, int32_t bpt, int32_t sps, int64_t n, int dtype) {
+  if (!c) return FT8_E_ARG;
+  if (dtype < FT8_F32 || dtype > FT8_I16) return fail(c, FT8_E_ARG, "unknown sample dtype");
+  Geo g;
+  std::string why;
+  int rc = geometry(fs, bpt, sps, n, &g, &why);
+  if (rc) return fail(c, rc, why);
+  DeviceGuard dg(c->device);
+  StftLaunch L{};
+  if ((rc = get_plan(c, g.nfft, is_cplx_dtype(dtype), is_f64_dtype(dtype), g.nperseg, &L.plan))) return rc;
+  if (L.plan.blue) return FT8_STFT_CHIRPZ;
+  if (L.plan.dft) return FT8_STFT_DFT;
+  L.dtype = dtype;
+  L.nfft = g.nfft;
+  L.nperseg = g.nperseg;
+  L.hop = g.hop;
+  L.slot_stride = 2;  // the packed kernel's only stride condition (even) is the caller's
+  return stft3840_eligible(L) ? FT8_STFT_PACKED3840 : FT8_STFT_STOCKHAM;
 }
 
 int ft8_sync_select(ft8_ctx* c, const void* d_wf, int wf_f64, int32_t n_slots, int32_t T, int32_t F,

@@ -12,8 +12,9 @@ namespace ft8 {
 constexpr int kWave = 64;
 constexpr int kMaxCandidates = 4096;   // LDS-resident selection (k_select)
 // LDS FFT limits (one (P + P/16 + 1)-point buffer per frame, 256 threads holding P / 256 values each
-// per stage; larger or non-2/3/5/7 lengths take the direct DFT): float32 P <= 10240 (87 KB), float64
-// P <= 8192 (139 KB)
+// per stage): float32 P <= 10240 (87 KB), float64 P <= 8192 (139 KB).  Larger or non-2/3/5/7 lengths
+// take the chirp-z transform (its power-of-two convolution on the same LDS FFT), or the direct DFT
+// where that convolution would not fit.
 constexpr int kMaxFftReal = 20480;     // float32 nfft of the real-input path (half-length FFT <= 10240)
 constexpr int kMaxFftComplex = 10240;  // float32 nfft of the complex-input path
 constexpr int kMaxFftP64 = 8192;       // float64: FFT points P (real nfft <= 16384, complex <= 8192)
@@ -33,13 +34,24 @@ struct cplx {
 
 // ---- STFT plan (host-built tables, device-resident) ----------------------------------------
 struct FftPlan {
-  int P;              // transform length (nfft/2 for real input, nfft for complex input; nfft if dft)
-  int dft;            // 1: no 2/3/5/7 factorisation (or odd real nfft): direct DFT, tw = W_nfft^m
+  int P;              // transform length (nfft/2 for real input, nfft for complex input; nfft if dft;
+                      // the convolution length M if blue)
+  int dft;            // 1: direct DFT (tw = W_nfft^m): lengths neither the Stockham plans nor the
+                      // chirp-z path take (nperseg above its LDS limit)
+  int blue;           // 1: chirp-z (Bluestein) transform, for an nfft with a prime factor above 7 or an
+                      // odd real nfft: every nfft-point DFT of a frame is a length-P (power of two)
+                      // circular convolution, run on the LDS Stockham FFT (stft.hip k_stft_blue)
   int nstages;
   int radix[16];
   const void* tw;     // W_P^m, m in [0, P): cplx<float> or cplx<double>
   const void* post;   // real path: W_N^k, k in [0, P]  (N = 2P)
+  // chirp-z (blue): the output bins of a frame are computed in blocks of B = P - nperseg + 1
+  int L, B, nblk;     // nperseg the plan is built for, bins per block, blocks covering [0, nfft)
+  const void* chirp;  // exp(-i pi k^2 / nfft), k in [0, nfft)
+  const void* hspec;  // [nblk][P]: FFT_P of block b's chirp filter conj(chirp(b B + m - (L - 1)))
 };
+constexpr int kMaxBlueP64 = 8192;       // chirp-z convolution length limits (the LDS FFT's)
+constexpr int kMaxBlueP32 = 8192;
 
 struct StftLaunch {
   const void* samples;

@@ -687,6 +687,101 @@ __global__ __launch_bounds__(kDftThreads) void k_stft_dft(StftArgs a) {
   else out[i] = 10.0 * log10(1e-12 + pw);
 }
 
+// ---- k_stft_blue: chirp-z (Bluestein) transform for lengths the Stockham plans cannot take ---------
+// (an nfft with a prime factor above 7, e.g. the reference drift test's 32 768 Hz: nfft 10 485 =
+// 3^2 x 5 x 233; an odd nfft with real input).  With c(k) = exp(-i pi k^2 / N), the frame's DFT is
+//   X[k] = c(k) sum_{n < L} a[n] conj(c(k - n)),   a[n] = c(n) w[n] x[n],
+// a linear convolution of the L windowed samples with a chirp filter.  Output bins are taken in
+// blocks of B = P - L + 1 (overlap-save): block b's bins k0 + t (k0 = b B, t < B) are samples
+// t + L - 1 of the length-P circular convolution of a with h_b[m] = conj(c(k0 + m - (L - 1))),
+// m < B + L - 1, which no wrap-around reaches.  One workgroup per (slot, frame, block): a -> FFT_P
+// (LDS Stockham, P a power of two) -> times FFT_P(h_b) (precomputed per plan) -> inverse FFT_P (the
+// forward stages on the conjugate) -> c(k) y / P.  O(P log P) per block instead of the direct DFT's
+// O(L) per bin: for the 32 768 Hz complex128 geometry (P 8192, L 5242, two blocks cover the kept
+// f >= 0 half) ~2 MFLOP per frame against ~220.
+template <typename InT, bool CPLX, typename CT>
+struct BlueSrc {
+  const InT* x;       // frame start (complex: InT = CT pairs)
+  const CT* w;        // window
+  const cplx<CT>* c;  // chirp
+  int L;
+  __device__ __forceinline__ cplx<CT> operator()(int n) const {
+    if (n >= L) return {(CT)0, (CT)0};
+    CT re, im = (CT)0;
+    if constexpr (CPLX) {
+      const CT* xc = reinterpret_cast<const CT*>(x);
+      re = xc[2 * n];
+      im = xc[2 * n + 1];
+    } else if constexpr (sizeof(CT) == 4) {
+      re = load_f32<InT>(x, n);
+    } else {
+      re = (CT)x[n];
+    }
+    const cplx<CT> z = {w[n] * re, w[n] * im};
+    return cmul(z, c[n]);
+  }
+};
+
+struct BlueArgs {
+  StftArgs s;
+  int L, B, blk0, nblk_run;  // blocks blk0 .. blk0 + nblk_run - 1 cover the kept bins
+  const void* chirp;
+  const void* hspec;
+};
+
+template <typename InT, bool CPLX, typename CT, int MAXV>
+__global__ __launch_bounds__(kThreads, 1) void k_stft_blue(BlueArgs b) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  cplx<CT>* buf = reinterpret_cast<cplx<CT>*>(smem);
+  const StftArgs& a = b.s;
+  // XCD-aware order as k_stft: each XCD takes a contiguous run of (slot, frame, block) triples, so a
+  // frame's blocks and its neighbours (overlapping samples) share one L2
+  const int nt = a.nt_out;
+  const int r = (int)(blockIdx.x & 7) * a.per_xcd + (int)(blockIdx.x >> 3);
+  if (r >= nt * a.n_slots * b.nblk_run) return;
+  const int blk = b.blk0 + r % b.nblk_run;
+  const int sf = r / b.nblk_run;
+  const int slot = sf / nt, fi = sf - slot * nt;
+  const int frame = a.t_lo + fi;
+  const InT* xs = reinterpret_cast<const InT*>(a.samples) +
+                  (int64_t)slot * a.slot_stride * (CPLX ? 2 : 1) + (int64_t)frame * a.hop * (CPLX ? 2 : 1);
+  const cplx<CT>* chirp = reinterpret_cast<const cplx<CT>*>(b.chirp);
+  BlueSrc<InT, CPLX, CT> src{xs, reinterpret_cast<const CT*>(a.window), chirp, b.L};
+  const cplx<CT>* tw = reinterpret_cast<const cplx<CT>*>(a.tw);
+  const int P = a.P;
+  // forward FFT of a
+  int Ns = 1;
+  run_stage<MAXV, true>(a.radix[0], buf, P, Ns, tw, src);
+  Ns *= a.radix[0];
+  for (int st = 1; st < a.nstages; ++st) {
+    run_stage<MAXV, false>(a.radix[st], buf, P, Ns, tw, src);
+    Ns *= a.radix[st];
+  }
+  // times the block's filter spectrum, conjugated: the forward stages then give P conj(y)
+  const cplx<CT>* H = reinterpret_cast<const cplx<CT>*>(b.hspec) + (int64_t)blk * P;
+  for (int k = threadIdx.x; k < P; k += kThreads) {
+    const cplx<CT> y = cmul(buf[pidx(k)], H[k]);
+    buf[pidx(k)] = {y.x, -y.y};
+  }
+  __syncthreads();
+  Ns = 1;
+  for (int st = 0; st < a.nstages; ++st) {
+    run_stage<MAXV, false>(a.radix[st], buf, P, Ns, tw, src);
+    Ns *= a.radix[st];
+  }
+  // bins of this block inside the kept range -> dB row (argmax requests reduce the rows afterwards)
+  const int k0 = blk * b.B;
+  const int lo = max(k0, a.f_lo), hi = min(k0 + b.B, a.f_lo + a.nf_out);
+  const CT inv = (CT)1 / (CT)P, scale = (CT)a.scale;
+  CT* out = reinterpret_cast<CT*>(a.out) + ((int64_t)slot * a.nt_out + fi) * a.nf_out;
+  for (int k = lo + (int)threadIdx.x; k < hi; k += kThreads) {
+    const cplx<CT> v = buf[pidx(k - k0 + b.L - 1)];
+    const cplx<CT> X = cmul(chirp[k], cplx<CT>{v.x * inv, -v.y * inv});
+    const CT pw = (X.x * X.x + X.y * X.y) * scale;
+    out[k - a.f_lo] = db_of((CT)1e-12 + pw);
+  }
+}
+
 // np.argmax of each dB row [slot][frame][nf] (the direct-DFT path's argmax): one wave per row
 template <typename CT>
 __global__ __launch_bounds__(kWave) void k_row_argmax(const CT* rows, int nf, int64_t n_rows, int32_t* idx) {
@@ -718,6 +813,36 @@ hipError_t launch_dft(const StftLaunch& L, const StftArgs& a, hipStream_t s) {
   }
   const int nbb = (a.nf_out + kDftThreads - 1) / kDftThreads;
   hipLaunchKernelGGL(kern, dim3((unsigned)(nbb * a.nt_out), (unsigned)L.n_slots), dim3(kDftThreads), lds, s, a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || !L.argmax) return e;
+  const int64_t rows = (int64_t)a.nt_out * L.n_slots;
+  hipLaunchKernelGGL(k_row_argmax<CT>, dim3((unsigned)rows), dim3(kWave), 0, s, reinterpret_cast<const CT*>(a.out),
+                     a.nf_out, rows, L.argmax);
+  return hipGetLastError();
+}
+
+template <typename InT, bool CPLX, typename CT>
+hipError_t launch_blue(const StftLaunch& L, const StftArgs& a, hipStream_t s) {
+  BlueArgs b{};
+  b.s = a;
+  b.s.argmax = nullptr;  // the rows are written; an argmax request reduces them below
+  b.L = L.plan.L;
+  b.B = L.plan.B;
+  b.blk0 = a.f_lo / b.B;
+  b.nblk_run = (a.f_lo + a.nf_out - 1) / b.B - b.blk0 + 1;
+  b.chirp = L.plan.chirp;
+  b.hspec = L.plan.hspec;
+  const int64_t units = (int64_t)a.nt_out * L.n_slots * b.nblk_run;
+  b.s.per_xcd = (int)((units + 7) / 8);
+  const size_t lds = (size_t)(a.P + a.P / 16 + 1) * sizeof(cplx<CT>);
+  if (a.P > kThreads * 32 || L.plan.L > a.P) return hipErrorInvalidValue;
+  auto kern = a.P <= kThreads * 16 ? k_stft_blue<InT, CPLX, CT, 16> : k_stft_blue<InT, CPLX, CT, 32>;
+  if (lds > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(kern, dim3((unsigned)(8 * b.s.per_xcd)), dim3(kThreads), lds, s, b);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || !L.argmax) return e;
   const int64_t rows = (int64_t)a.nt_out * L.n_slots;
@@ -778,6 +903,16 @@ hipError_t launch_stft(const StftLaunch& L, hipStream_t s) {
   a.n_slots = L.n_slots;
   a.per_xcd = (int)(((int64_t)a.nt_out * L.n_slots + 7) / 8);
   if (a.nt_out <= 0 || a.nf_out <= 0 || L.n_slots <= 0) return hipSuccess;
+  if (L.plan.blue) {
+    switch (L.dtype) {
+      case FT8_F32: return launch_blue<float, false, float>(L, a, s);
+      case FT8_I16: return launch_blue<int16_t, false, float>(L, a, s);
+      case FT8_F64: return launch_blue<double, false, double>(L, a, s);
+      case FT8_C64: return launch_blue<float, true, float>(L, a, s);
+      case FT8_C128: return launch_blue<double, true, double>(L, a, s);
+      default: return hipErrorInvalidValue;
+    }
+  }
   if (L.plan.dft) {
     a.argmax = nullptr;  // the DFT kernel writes dB rows; launch_dft reduces them to the argmax
     switch (L.dtype) {

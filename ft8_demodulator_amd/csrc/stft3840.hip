@@ -364,7 +364,7 @@ __global__ __launch_bounds__(kThreads38) void k_stft3840p(Args a) {
 }  // namespace
 
 bool stft3840_eligible(const StftLaunch& L) {
-  return !L.argmax && !L.plan.dft && (L.dtype == FT8_F32 || L.dtype == FT8_I16) && L.nfft == 2 * kP &&
+  return !L.argmax && !L.plan.dft && !L.plan.blue && (L.dtype == FT8_F32 || L.dtype == FT8_I16) && L.nfft == 2 * kP &&
          L.nperseg == kP && L.hop == 960 && L.plan.P == kP && (L.slot_stride % 2) == 0;
 }
 

@@ -132,6 +132,17 @@ int ft8_geometry(int32_t sample_rate, int32_t bins_per_tone, int32_t steps_per_s
 int ft8_stft(ft8_ctx* ctx, const void* d_samples, int dtype, int64_t n_samples, int32_t n_slots,
              int64_t slot_stride, const ft8_params* p, void* d_wf, void* stream);
 
+/* Which transform ft8_stft / ft8_decode_batch runs for a geometry (introspection for tests and
+ * tuning): FT8_STFT_STOCKHAM (LDS mixed-radix FFT), FT8_STFT_PACKED3840 (the production 12 kHz
+ * kernel), FT8_STFT_CHIRPZ (Bluestein: nfft with a prime factor above 7, or odd with real input),
+ * FT8_STFT_DFT (direct DFT: what neither FFT path takes); negative FT8_E_* on a bad geometry. */
+#define FT8_STFT_STOCKHAM 0
+#define FT8_STFT_PACKED3840 1
+#define FT8_STFT_CHIRPZ 2
+#define FT8_STFT_DFT 3
+int ft8_stft_method(ft8_ctx* ctx, int32_t sample_rate, int32_t bins_per_tone, int32_t steps_per_symbol,
+                    int64_t n_samples, int dtype);
+
 /* ---- stage 2: Costas sync score grid + candidate selection ---------------------------------
  * Replaces ft8_sync_score / ft8_find_candidates (ft8_decode.py:47-149).  d_wf as produced by
  * ft8_stft: [n_slots][T][F] (row stride F, slot stride T*F), float32 (wf_f64=0) or float64.

@@ -32,16 +32,29 @@ def test_short_input_empty(gpu):
     assert s.shape == (1, 0) and f.size == 0 and t.size == 0
 
 
-@pytest.mark.parametrize("fs,bpt,sps,cplx,dt", [
-    (32768, 2, 2, False, np.float64),   # nfft 10485: odd and a prime factor 233 (reference test rate)
-    (32768, 2, 8, True, np.complex128),
-    (11025, 3, 2, False, np.float32),   # nfft 5292 = 2^2 3^3 7^2 ... P = 2646 = 2 3^3 7^2: FFT path
-    (9973, 1, 2, False, np.float32),    # prime-ish rate: nfft 1595 = 5 x 11 x 29, odd real
+ST, P38, CZ, DFT = 0, 1, 2, 3  # ft8_stft_method: Stockham, packed 3840, chirp-z, direct DFT
+
+
+@pytest.mark.parametrize("fs,bpt,sps,cplx,dt,method", [
+    (32768, 2, 2, False, np.float64, CZ),    # nfft 10485 = 3^2 5 233: odd, a prime factor 233 (reference test rate)
+    (32768, 2, 8, True, np.complex128, CZ),  # the reference drift test's geometry
+    (32768, 2, 2, False, np.float32, CZ),
+    (11025, 3, 2, False, np.float32, ST),    # nfft 5292 = 2^2 3^3 7^2 ... P = 2646 = 2 3^3 7^2: FFT path
+    (9973, 1, 2, False, np.float32, CZ),     # prime-ish rate: nfft 1595 = 5 x 11 x 29, odd real
+    (9973, 2, 2, True, np.complex64, CZ),    # nfft 3191, a prime
+    (12000, 10, 10, False, np.float32, ST),  # nfft 19200: the 40-values-per-thread LDS FFT (P 9600)
+    (12000, 5, 2, True, np.complex64, ST),   # complex nfft 9600 in (8192, 10240]: the same variant
+    (12000, 2, 2, False, np.float32, P38),   # the production geometry
 ])
-def test_any_fft_length_matches_scipy(gpu, oracle, fs, bpt, sps, cplx, dt):
-    """Lengths without a 2/3/5/7 factorisation (or odd real nfft) take the direct-DFT kernel; every
-    geometry matches scipy within the same tolerances as the golden cases."""
-    from ft8_demodulator_amd import calculate_spectrogram
+def test_any_fft_length_matches_scipy(gpu, oracle, fs, bpt, sps, cplx, dt, method):
+    """Lengths without a 2/3/5/7 factorisation (or odd real nfft) take the chirp-z transform (or the
+    direct DFT, where the chirp-z convolution would not fit the LDS FFT); every geometry matches
+    scipy within the same tolerances as the golden cases."""
+    from ft8_demodulator_amd import _lib, calculate_spectrogram
+    code = {np.float32: _lib.FT8_F32, np.float64: _lib.FT8_F64, np.complex64: _lib.FT8_C64,
+            np.complex128: _lib.FT8_C128}[dt]
+    ctx = _lib.context()
+    assert _lib.lib().ft8_stft_method(ctx.handle, fs, bpt, sps, int(0.16 * fs) * 12, code) == method
     rng = np.random.default_rng(fs + sps)
     n = int(0.16 * fs) * 12
     x = rng.normal(size=n) + (1j * rng.normal(size=n) if cplx else 0)
