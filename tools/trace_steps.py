@@ -38,8 +38,11 @@ def main():
     rows = []
     with open(a.trace) as f:
         for r in csv.DictReader(f):
-            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"])))
-    rows.sort()
+            rows.append((int(r["Dispatch_Id"]), int(r["Start_Timestamp"]), int(r["End_Timestamp"]),
+                         short(r["Kernel_Name"])))
+    # submission order: a kernel's start timestamp can precede its predecessor's end (and even
+    # start) by a few microseconds in the trace, so sorting by start misorders steps
+    rows = [r[1:] for r in sorted(rows)]
     ft8 = [r for r in rows if r[2].startswith("k_")]
     # decode steps: a k_stft followed (next ft8 kernels) by score, select, llr, bp, compact
     steps = []
