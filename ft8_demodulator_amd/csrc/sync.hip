@@ -239,29 +239,18 @@ __device__ __forceinline__ void s2_load(const float* wf, int T, int F, int a0, i
 }
 
 // One workgroup: 128 grid columns x 22 grid rows of one slot.  The three Costas bands of the
-// waterfall the candidates read are staged ONE AT A TIME, band m + 1's global loads in flight while
-// band m is scored, and each wave keeps its rows' two-column partial sums in registers across the
-// bands, so every score accumulates its 75 terms in the reference's order (band, symbol, tone-1,
-// tone+1, time-1, time+1).
-//
-// A band is not staged as the dB values p but as their differences (computed once per staged value
-// instead of once per candidate that reads them):
-//   D(r, x) = p(r, x) - p(r, x - bpt)     (frequency: the tone-1 term of a tone at x)
-//   V(r, x) = p(r, x) - p(r - sps, x)     (time: the time-1 term of a symbol at row r)
-// Every term of ft8_sync_score is one of them with a sign: tone-1 = D(r, x), tone+1 = p(x) -
-// p(x + bpt) = -D(r, x + bpt), time-1 = V(r, x), time+1 = -V(r + sps, x).  IEEE rounding is sign-
-// symmetric, so RN(q - p) = -RN(p - q) exactly, and score + (-d) is score - d exactly: the running
-// float32 sums are bit-identical to the reference's, with one packed add per term instead of a
-// subtraction and an add (VALU was 80 % busy with the plain form).
+// waterfall the candidates read are staged into LDS ONE AT A TIME (22 KB at bpt = sps = 2, so four
+// workgroups -- 32 waves -- share a CU), band m + 1's global loads in flight while band m is scored;
+// each wave keeps its rows' two-column partial sums in registers across the bands, so every score
+// still accumulates its 75 terms in the reference's order (band, symbol, tone-1, tone+1, time-1,
+// time+1).
 template <int BPT, int SPS, bool COMPACT>
 __global__ __launch_bounds__(kS2Threads) void k_score2(ScoreArgs a) {
   static_assert(kS2TW == kSegCols, "a workgroup's columns are one score segment");
-  static_assert(BPT <= 4, "D reads the previous float4 of a row");
   using G = S2Geom<BPT, SPS>;
-  constexpr int P = G::P, Q = G::Q;
+  constexpr int P = G::P;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  float* tD = reinterpret_cast<float*>(smem);   // p while staging, then D
-  float* tV = tD + G::kFloats;                   // V
+  float* tile = reinterpret_cast<float*>(smem);
   // workgroup -> (slot, row tile, column tile); slot % 8 == workgroup id % 8 keeps a slot on one XCD
   const int id = blockIdx.x;
   const int per = a.n_bands * a.n_ctiles;
@@ -293,87 +282,41 @@ __global__ __launch_bounds__(kS2Threads) void k_score2(ScoreArgs a) {
 #pragma unroll 1
   for (int m = 0; m < 3; ++m) {
     if (m > 0) __syncthreads();  // every wave has scored band m - 1
-    // ---- stage p, then turn it into D and V (register-held between the barriers)
     if (vec) {
 #pragma unroll
       for (int it = 0; it < G::kIter; ++it) {
         const int idx = (int)threadIdx.x + it * kS2Threads;
-        if (idx < G::H * Q) reinterpret_cast<float4*>(tD)[idx] = v[it];
-      }
-      __syncthreads();
-      float4 dv[G::kIter], vv[G::kIter];
-#pragma unroll
-      for (int it = 0; it < G::kIter; ++it) {
-        const int idx = (int)threadIdx.x + it * kS2Threads;
-        const int rw = idx / Q, q4 = idx - rw * Q;
-        const float4 own = v[it];
-        const float4 prev = (idx < G::H * Q && q4 > 0) ? reinterpret_cast<const float4*>(tD)[idx - 1]
-                                                       : make_float4(0.f, 0.f, 0.f, 0.f);
-        const float4 up = (idx < G::H * Q && rw >= SPS) ? reinterpret_cast<const float4*>(tD)[idx - SPS * Q]
-                                                        : make_float4(0.f, 0.f, 0.f, 0.f);
-        const float e[8] = {prev.x, prev.y, prev.z, prev.w, own.x, own.y, own.z, own.w};
-        dv[it] = make_float4(own.x - e[4 - BPT], own.y - e[5 - BPT], own.z - e[6 - BPT], own.w - e[7 - BPT]);
-        vv[it] = make_float4(own.x - up.x, own.y - up.y, own.z - up.z, own.w - up.w);
+        if (idx < G::H * G::Q) reinterpret_cast<float4*>(tile)[idx] = v[it];
       }
       if (m < 2) s2_load<BPT, SPS>(wf, a.T, a.F, a0, c0, m + 1, v);  // in flight while band m is scored
-      __syncthreads();  // every read of p is done
-#pragma unroll
-      for (int it = 0; it < G::kIter; ++it) {
-        const int idx = (int)threadIdx.x + it * kS2Threads;
-        if (idx < G::H * Q) {
-          reinterpret_cast<float4*>(tD)[idx] = dv[it];
-          reinterpret_cast<float4*>(tV)[idx] = vv[it];
-        }
-      }
     } else {
       for (int i = threadIdx.x; i < G::kFloats; i += kS2Threads) {
         const int rr = i / P, cc = i - rr * P;
         const int row = a0 + 36 * m * SPS - SPS + rr, col = c0 + cc;
         float x = 0.0f;
         if (row >= 0 && row < a.T && col < a.F) x = wf[(int64_t)row * a.F + col];
-        tV[i] = x;  // p staged in the V region
-      }
-      __syncthreads();
-      float dd[(G::kFloats + kS2Threads - 1) / kS2Threads], vd[(G::kFloats + kS2Threads - 1) / kS2Threads];
-#pragma unroll
-      for (int it = 0; it < (G::kFloats + kS2Threads - 1) / kS2Threads; ++it) {
-        const int i = (int)threadIdx.x + it * kS2Threads;
-        const int rr = i / P, cc = i - rr * P;
-        const bool in = i < G::kFloats;
-        const float x = in ? tV[i] : 0.0f;
-        dd[it] = x - ((in && cc >= BPT) ? tV[i - BPT] : 0.0f);
-        vd[it] = x - ((in && rr >= SPS) ? tV[i - SPS * P] : 0.0f);
-      }
-      __syncthreads();
-#pragma unroll
-      for (int it = 0; it < (G::kFloats + kS2Threads - 1) / kS2Threads; ++it) {
-        const int i = (int)threadIdx.x + it * kS2Threads;
-        if (i < G::kFloats) {
-          tD[i] = dd[it];
-          tV[i] = vd[it];
-        }
+        tile[i] = x;
       }
     }
     __syncthreads();
-    // ---- score band m: each term one D or V pair (8-byte LDS read) and one packed add
 #pragma unroll
     for (int u = 0; u < kS2Rows; ++u) {
       const int j = w + u * kS2Waves;        // wave-uniform
       if (j >= rows) continue;
       const int lo = floordiv(a0 + j, SPS) + 36 * m;  // block index of the band's first Costas symbol
-      const float* dB = tD + j * P + 2 * lane;
-      const float* vB = tV + j * P + 2 * lane;
+      const float* tb = tile + j * P + 2 * lane;
       if (lo >= 0 && lo <= nb - 7) {
         // every symbol of the band and all its neighbours in range: straight-line code
         // (25 differences, in the reference order)
 #pragma unroll
         for (int k = 0; k < 7; ++k) {
           const int tone = kCostasC[k];
-          const int o = (k + 1) * SPS * P + tone * BPT;
-          if (tone > 0) score[u] += ld2<BPT>(dB + o);
-          if (tone < 7) score[u] -= ld2<BPT>(dB + o + BPT);
-          if (k > 0) score[u] += ld2<BPT>(vB + o);
-          if (k < 6) score[u] -= ld2<BPT>(vB + o + SPS * P);
+          const float* rp = tb + (k + 1) * SPS * P + tone * BPT;
+          const f32x2 pw = ld2<BPT>(rp);
+          if (tone > 0) score[u] += pw - ld2<BPT>(rp - BPT);
+          if (tone < 7) score[u] += pw - ld2<BPT>(rp + BPT);
+          if (k > 0) score[u] += pw - ld2<BPT>(rp - SPS * P);
+          if (k < 6) score[u] += pw - ld2<BPT>(rp + SPS * P);
         }
         n[u] += 25;
       } else if (lo + 6 >= 0 && lo < nb) {
@@ -383,11 +326,12 @@ __global__ __launch_bounds__(kS2Threads) void k_score2(ScoreArgs a) {
           const int ba = lo + k;
           if (ba < 0 || ba >= nb) continue;
           const int tone = kCostasC[k];
-          const int o = (k + 1) * SPS * P + tone * BPT;
-          if (tone > 0) { score[u] += ld2<BPT>(dB + o); n[u]++; }
-          if (tone < 7) { score[u] -= ld2<BPT>(dB + o + BPT); n[u]++; }
-          if (k > 0 && ba > 0) { score[u] += ld2<BPT>(vB + o); n[u]++; }
-          if (k < 6 && ba + 1 < nb) { score[u] -= ld2<BPT>(vB + o + SPS * P); n[u]++; }
+          const float* rp = tb + (k + 1) * SPS * P + tone * BPT;
+          const f32x2 pw = ld2<BPT>(rp);
+          if (tone > 0) { score[u] += pw - ld2<BPT>(rp - BPT); n[u]++; }
+          if (tone < 7) { score[u] += pw - ld2<BPT>(rp + BPT); n[u]++; }
+          if (k > 0 && ba > 0) { score[u] += pw - ld2<BPT>(rp - SPS * P); n[u]++; }
+          if (k < 6 && ba + 1 < nb) { score[u] += pw - ld2<BPT>(rp + SPS * P); n[u]++; }
         }
       }
     }
@@ -444,16 +388,8 @@ hipError_t launch_score2(const SyncLaunch& L, const ScoreArgs& a0, hipStream_t s
   ScoreArgs a = a0;
   a.n_bands = (L.NT + kS2R - 1) / kS2R;
   a.n_ctiles = (L.NF + kS2TW - 1) / kS2TW;
-  const size_t lds = 2 * sizeof(float) * G::kFloats;  // D and V of one band (44 KB at bpt = sps = 2)
-  if (lds > 64 * 1024) {
-    static bool attr = false;
-    if (!attr) {
-      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_score2<BPT, SPS, COMPACT>),
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      if (e != hipSuccess) return e;
-      attr = true;
-    }
-  }
+  const size_t lds = sizeof(float) * G::kFloats;
+  static_assert(sizeof(float) * S2Geom<4, 4>::kFloats <= 64 * 1024, "one band fits the default LDS limit");
   const int groups = (L.n_slots + 7) / 8;
   const int64_t blocks = (int64_t)groups * 8 * a.n_bands * a.n_ctiles;
   hipLaunchKernelGGL((k_score2<BPT, SPS, COMPACT>), dim3((unsigned)blocks), dim3(kS2Threads), lds, s, a);
