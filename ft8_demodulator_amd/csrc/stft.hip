@@ -526,13 +526,13 @@ __global__ __launch_bounds__(kC38Threads, 2) void k_stftc3840(StftArgs a) {
       }
       dft16_half_t<CT>(v);
 #pragma unroll
-      for (int k = 0; k < 16; ++k) buf[pidx(16 * t + k)] = v[k];
+      for (int k = 0; k < 16; ++k) buf[17 * t + k] = v[k];  // pidx(16 t + k)
     }
     __syncthreads();
     // stage 2: radix 16, Ns = 16: buf[t + 240 r] -> twiddle W_256^(r k), k = t % 16 -> buf[(t/16) 256 + k + 16 r]
     if (s1) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) v[r] = buf[pidx(t + 240 * r)];
+      for (int r = 0; r < 16; ++r) v[r] = buf[pidx(t) + 255 * r];  // pidx(t + 240 r)
     }
     __syncthreads();
     if (s1) {
@@ -546,12 +546,12 @@ __global__ __launch_bounds__(kC38Threads, 2) void k_stftc3840(StftArgs a) {
       Dft<16, CT>::run(v);
       const int d0 = (t >> 4) * 256 + k;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) buf[pidx(d0 + 16 * r)] = v[r];
+      for (int r = 0; r < 16; ++r) buf[pidx(d0) + 17 * r] = v[r];  // pidx(d0 + 16 r)
     }
     __syncthreads();
     // stage 3: radix 15, Ns = 256: buf[t + 256 r] -> twiddle W_3840^(r t) -> X[t + 256 r]
 #pragma unroll
-    for (int r = 0; r < 15; ++r) v[r] = buf[pidx(t + 256 * r)];
+    for (int r = 0; r < 15; ++r) v[r] = buf[pidx(t) + 272 * r];  // pidx(t + 256 r)
     __syncthreads();  // the next frame's stage 1 may overwrite buf
     {
       cplx<CT> wr = s3;

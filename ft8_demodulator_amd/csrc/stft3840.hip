@@ -16,12 +16,12 @@
 // This file is built with packed math enabled and FMA contraction (Makefile); the FFT is not
 // pocketfft in either case, and tests bound the dB error (tests/test_gpu_stft.py).
 //
-// Work decomposition: 256 threads (four waves) per frame, one butterfly per thread per stage
-// (stage 1 on 120 threads, stage 2 on 240, stage 3 on 128), ping-pong LDS buffers, twiddles formed
-// in registers by recurrence from per-thread seeds; a workgroup walks a run of consecutive frames
-// of one slot and keeps the raw samples in registers, since a frame's second half is the next
-// frame's first half (each run reads (c + 1) / c of its samples), prefetching the next frame's new
-// samples.
+// Work decomposition: 256 threads (four waves) transform TWO frames per pass: stages 1 and 3 run
+// frame A on threads 0..127 and frame B on 128..255 (120 / 128 of each half busy), stage 2 both
+// frames' radix-8 butterfly j = t on 240 threads, the epilogue both frames' bins; one LDS image per
+// frame with every stage in place, twiddles formed in registers by recurrence from per-thread
+// seeds; a workgroup walks a run of consecutive frames of one slot, each thread loading its next
+// frame's raw samples as soon as stage 1 has consumed the current ones.
 #include "ft8_internal.h"
 
 namespace ft8 {
@@ -194,14 +194,18 @@ __device__ __forceinline__ f2 load_pair(const InT* x, int64_t n0) {
 }
 
 constexpr int kP = 1920;
-// four waves per frame: stage 2 one butterfly per thread, stages 1 and 3 on the first 120 / 128
-// threads, the epilogue on all (two waves with two stage-2 butterflies per thread: 0.185 vs 0.175 ms
-// per 256-slot launch; one LDS buffer needs 176 VGPRs at 128 threads)
+// four waves, TWO frames per pass (round 3): stage 1 and stage 3 run frame A on threads 0..127 and
+// frame B on 128..255, stage 2 does both frames' radix-8 butterfly j = t (sharing its twiddles), the
+// epilogue both frames' bins k = t + 256 i (sharing the post-twiddle recurrence).  One frame per
+// pass left stages 1 and 3 on 120 / 128 of the 256 threads -- two of the four waves waited at the
+// barrier through the two heaviest stages.
 constexpr int kThreads38 = 256;
-// frames per workgroup, 31 workgroups per slot at 186 frames (6: 0.168-0.171 ms vs 8: 0.172-0.178,
-// 4/5/12/16 no better, profiles/r2_s27/s28_*_ab.log)
+// frames per workgroup (three passes), 31 workgroups per 186-frame slot
 constexpr int kChunk = 6;
-static_assert(kThreads38 == 256 && kThreads38 >= 240, "stage 2: one radix-8 butterfly per thread (240)");
+static_assert(kThreads38 == 256 && kChunk % 2 == 0, "two frames per pass on 2 x 128 threads");
+// one LDS image per frame, every stage in place, with pidx padding (stage 1 writes with a
+// 16-complex stride across lanes: 128 B, 32-way bank conflicts unpadded)
+constexpr int kBuf = kP + (kP - 1) / 16;
 
 struct Args {
   const void* samples;
@@ -215,22 +219,28 @@ struct Args {
 };
 
 __device__ __forceinline__ int pidx(int i) { return i + (i >> 4); }
+// LDS accesses one ds_read_b64 / ds_write_b64 each (volatile): merged ds_read2_b64 / ds_write2_b64
+// move half the bytes per LDS cycle, and their 8-bit offsets made the compiler keep a base
+// register per pair of positions (~20 VGPRs of addresses live through the frame loop)
+typedef __attribute__((address_space(3))) f2 lds_f2;
+__device__ __forceinline__ f2 lds_ld(const f2* p) { return *(const volatile lds_f2*)p; }
+__device__ __forceinline__ void lds_st(f2* p, f2 v) { *(volatile lds_f2*)p = v; }
 
 template <typename InT>
 __global__ __launch_bounds__(kThreads38) void k_stft3840p(Args a) {
-  // bufA is read and written with pidx padding: the stage-1 writes go out with a 16-complex stride
-  // across lanes (128 B: 32-way bank conflicts unpadded)
-  __shared__ f2 bufA[kP + kP / 16 + 1];
-  __shared__ f2 bufB[kP];
+  __shared__ f2 buf[2][kBuf];  // frame A, frame B
+  __shared__ f2 wl[kP / 2];    // the window as pairs (w[2n], w[2n+1]): 39.4 KB in all, four workgroups per CU
   const int t = threadIdx.x;
+  const int role = t >> 7;  // stages 1 and 3: the frame this thread works on (A = 0, B = 1)
+  const int u = t & 127;    // ... and its index there
   const int chunks = (a.nt_out + kChunk - 1) / kChunk;
   const int slot = blockIdx.x / chunks;
   const int c = blockIdx.x - slot * chunks;
   const int f_begin = c * kChunk, f_end = min(a.nt_out, f_begin + kChunk);
-  // twiddle seeds: stage 2 W_128^k (k = t % 16), stage 3 W_1920^t, epilogue W_3840^(f_lo + t) and
-  // its 128-bin step; their powers are formed by complex recurrence each frame (relative error
+  // twiddle seeds: stage 2 W_128^k (k = t % 16), stage 3 W_1920^u, epilogue W_3840^(f_lo + t) and
+  // its 256-bin step; their powers are formed by complex recurrence each pass (relative error
   // ~15 ulp, far inside the dB tolerance)
-  f2 s2 = a.tw[15 * (t & 15)], s3 = a.tw[t];
+  f2 s2 = a.tw[15 * (t & 15)], s3 = a.tw[u];
   const bool rec_post = a.f_lo + a.nf_out <= kP;
   const bool full = a.f_lo == 0 && a.nf_out == kP;  // every f >= 0 bin kept (no band mask)
   // 10 log10(v) = (10 log10 2) log2(v): v_log_f32 on a normal argument (v >= 1e-12)
@@ -239,69 +249,79 @@ __global__ __launch_bounds__(kThreads38) void k_stft3840p(Args a) {
   const f2 pstep = a.post[kThreads38];
   const f2 qscale = splat(0.25f * a.scale);  // |2 X|^2 / 4 / (sum w)^2 (powers of two: exact)
 
-  // the window of the thread's 8 stage-1 pairs, in registers
-  const bool s1 = t < 120;
-  f2 win[8];
-#pragma unroll
-  for (int r = 0; r < 8; ++r) win[r] = s1 ? *reinterpret_cast<const f2*>(a.window + 2 * (t + 120 * r)) : splat(0.0f);
+  for (int n = t; n < kP / 2; n += kThreads38) wl[n] = *reinterpret_cast<const f2*>(a.window + 2 * n);
+  const bool s1 = u < 120;
   const InT* xs = reinterpret_cast<const InT*>(a.samples) + (int64_t)slot * a.slot_stride;
-  f2 raw[8];  // raw pairs (x[2n], x[2n+1]), n = t + 120 r, of the current frame
-  {
-    const int64_t base = (int64_t)(a.t_lo + f_begin) * 960;
+  // raw pairs (x[2n], x[2n+1]), n = u + 120 r, of this thread's frame of the pass; loaded for the
+  // next pass as soon as stage 1 has consumed them
+  f2 raw[8];
+  auto load_raw = [&](int fr) {
+    const int64_t base = (int64_t)(a.t_lo + fr) * 960;
 #pragma unroll
-    for (int r = 0; r < 8; ++r) raw[r] = s1 ? load_pair<InT>(xs, base + 2 * (t + 120 * r)) : splat(0.0f);
-  }
-  for (int f = f_begin; f < f_end; ++f) {
-    // re-opaque the seeds so the per-frame twiddle powers are not hoisted into ~50 live registers
+    for (int r = 0; r < 8; ++r) raw[r] = load_pair<InT>(xs, base + 2 * (u + 120 * r));
+  };
+  if (s1 && f_begin + role < f_end) load_raw(f_begin + role);
+  for (int f = f_begin; f < f_end; f += 2) {
+    // re-opaque the seeds so the per-pass twiddle powers are not hoisted into ~50 live registers
     asm volatile("" : "+v"(s2), "+v"(s3), "+v"(p0));
-    // prefetch the next frame's 4 new pairs (n + 480 = t + 120 (r + 4))
-    f2 nx[4];
-    const bool more = f + 1 < f_end;
-    if (s1 && more) {
-      const int64_t base = (int64_t)(a.t_lo + f + 1) * 960;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) nx[r] = load_pair<InT>(xs, base + 2 * (t + 120 * (r + 4)));
-    }
-    // stage 1: radix 16, Ns = 1: inputs z[t + 120 r] (r >= 8 is zero padding) -> bufA[16 t + k]
-    __syncthreads();  // the previous frame's epilogue has finished reading bufA
-    if (s1) {
+    const bool haveB = f + 1 < f_end;        // workgroup-uniform
+    const bool mine = role == 0 || haveB;    // wave-uniform
+    f2* const img = buf[role];
+    // stage 1: radix 16, Ns = 1: inputs z[u + 120 r] (r >= 8 is zero padding) -> img[16 u + k]
+    __syncthreads();  // the previous pass's epilogue has finished reading both images
+    if (s1 && mine) {
       f2 z[8], y[16];
 #pragma unroll
-      for (int r = 0; r < 8; ++r) z[r] = win[r] * raw[r];
+      for (int r = 0; r < 8; ++r) z[r] = lds_ld(&wl[u + 120 * r]) * raw[r];
       dft16_half(z, y);
 #pragma unroll
-      for (int k = 0; k < 16; ++k) bufA[pidx(16 * t + k)] = y[k];
+      for (int k = 0; k < 16; ++k) lds_st(&img[17 * u + k], y[k]);  // pidx(16 u + k)
+      if (f + 2 + role < f_end) load_raw(f + 2 + role);  // in flight through stages 2, 3 and the epilogue
     }
     __syncthreads();
-    // stage 2: radix 8, Ns = 16: j = t (j < 240)
+    // stage 2: radix 8, Ns = 16: butterfly j = t (j < 240) of both frames
     {
       const int j = t;
+      f2 va[8], vb[8];
       if (j < 240) {
-        f2 v[8];
+        auto bfly = [&](const f2* img_, f2* v) {
 #pragma unroll
-        for (int r = 0; r < 8; ++r) v[r] = bufA[pidx(j + 240 * r)];
-        if ((j & 15) != 0) {
-          f2 w = s2;  // W_128^(r k)
+          for (int r = 0; r < 8; ++r) v[r] = lds_ld(&img_[pidx(j) + 255 * r]);  // pidx(j + 240 r)
+          if ((j & 15) != 0) {
+            f2 w = s2;  // W_128^(r k)
 #pragma unroll
-          for (int r = 1; r < 8; ++r) {
-            v[r] = cmul(v[r], w);
-            if (r < 7) w = cmul(w, s2);
+            for (int r = 1; r < 8; ++r) {
+              v[r] = cmul(v[r], w);
+              if (r < 7) w = cmul(w, s2);
+            }
           }
-        }
-        dft8(v);
+          dft8(v);
+        };
+        bfly(buf[0], va);
+        // frame B's reads after frame A's butterfly: interleaving the two needs ~100 more VGPRs
+        asm volatile("" : "+v"(s2) : : "memory");  // and its twiddle powers recomputed, not kept
+        if (haveB) bfly(buf[1], vb);
+      }
+      __syncthreads();  // every stage-2 read of the images is done: write in place
+      if (j < 240) {
         const int d0 = (j >> 4) * 128 + (j & 15);
 #pragma unroll
-        for (int r = 0; r < 8; ++r) bufB[d0 + 16 * r] = v[r];
+        for (int r = 0; r < 8; ++r) lds_st(&buf[0][pidx(d0) + 17 * r], va[r]);  // pidx(d0 + 16 r)
+        if (haveB) {
+#pragma unroll
+          for (int r = 0; r < 8; ++r) lds_st(&buf[1][pidx(d0) + 17 * r], vb[r]);
+        }
       }
     }
     __syncthreads();
-    // stage 3: radix 15, Ns = 128: j = t -> natural order into bufA
-    if (t < 128) {
+    // stage 3: radix 15, Ns = 128: j = u, natural order, in place (a thread writes the 15 positions
+    // it read)
+    if (mine) {
       f2 v[15], y[15];
 #pragma unroll
-      for (int r = 0; r < 15; ++r) v[r] = bufB[t + 128 * r];
-      if (t != 0) {
-        f2 w = s3;  // W_1920^(r t)
+      for (int r = 0; r < 15; ++r) v[r] = lds_ld(&img[pidx(u) + 136 * r]);  // pidx(u + 128 r)
+      if (u != 0) {
+        f2 w = s3;  // W_1920^(r u)
 #pragma unroll
         for (int r = 1; r < 15; ++r) {
           v[r] = cmul(v[r], w);
@@ -310,52 +330,51 @@ __global__ __launch_bounds__(kThreads38) void k_stft3840p(Args a) {
       }
       dft15(v, y);
 #pragma unroll
-      for (int r = 0; r < 15; ++r) bufA[pidx(t + 128 * r)] = y[r];
+      for (int r = 0; r < 15; ++r) lds_st(&img[pidx(u) + 136 * r], y[r]);
     }
     __syncthreads();
     // epilogue: real-signal spectrum X[k] = (s - i W_N^k d) / 2 with s = Z[k] + conj Z[P-k],
-    // d = Z[k] - conj Z[P-k]; power, dB, kept bins
-    float* out = a.out + ((int64_t)slot * a.nt_out + f) * a.nf_out;
+    // d = Z[k] - conj Z[P-k]; power, dB, kept bins -- frame A then frame B per bin block
+    const int nfr = haveB ? 2 : 1;
     if (full) {
       // k and P - k share s and d: since W_N^(P-k) = -conj(W_N^k), 2 X[P-k] = conj(s + i W d)... the
       // two spectra are (s.x + wd.y, s.y - wd.x) and (s.x - wd.y, -(s.y + wd.x)) for wd = W_N^k d;
       // their real parts and imaginary parts are formed side by side, so both powers come from one
       // packed multiply-add
-      f2 pw_k = p0;  // W_3840^k, k = t + 128 j
+      f2 pw_k = p0;  // W_3840^k, k = t + 256 i
       for (int k = t; k <= kP / 2; k += kThreads38) {
-        const f2 A = bufA[pidx(k)];
-        const f2 B = bufA[pidx(k == 0 ? 0 : kP - k)];
-        const f2 sm = add_cj(A, B), df = sub_cj(A, B);
-        const f2 wd = cmul(pw_k, df);
+        const f2 wk = pw_k;
         pw_k = cmul(pw_k, pstep);
-        const f2 re = re_pm(sm, wd), im = im_mp(sm, wd);   // (X1.x, X2.x), (X1.y, -X2.y)
-        const f2 p = (re * re + im * im) * qscale + splat(1e-12f);
-        const float d1 = kDb * __builtin_amdgcn_logf(p.x), d2 = kDb * __builtin_amdgcn_logf(p.y);
-        out[k] = d1;
-        if (k != 0 && k != kP / 2) out[kP - k] = d2;
+        for (int q = 0; q < nfr; ++q) {
+          const f2 A = lds_ld(&buf[q][pidx(k)]);
+          const f2 B = lds_ld(&buf[q][pidx(k == 0 ? 0 : kP - k)]);
+          const f2 sm = add_cj(A, B), df = sub_cj(A, B);
+          const f2 wd = cmul(wk, df);
+          const f2 re = re_pm(sm, wd), im = im_mp(sm, wd);   // (X1.x, X2.x), (X1.y, -X2.y)
+          const f2 p = (re * re + im * im) * qscale + splat(1e-12f);
+          const float d1 = kDb * __builtin_amdgcn_logf(p.x), d2 = kDb * __builtin_amdgcn_logf(p.y);
+          float* out = a.out + ((int64_t)slot * a.nt_out + f + q) * a.nf_out;
+          out[k] = d1;
+          if (k != 0 && k != kP / 2) out[kP - k] = d2;
+        }
       }
     } else {
-      f2 pw_k = p0;  // W_3840^k for k = f_lo + i (recurrence over i += 128)
+      f2 pw_k = p0;  // W_3840^k for k = f_lo + i (recurrence over i += 256)
       for (int i = t; i < a.nf_out; i += kThreads38) {
         const int k = a.f_lo + i;
         const int kk = (k <= kP) ? k : 2 * kP - k;
-        const f2 A = bufA[pidx(kk == kP ? 0 : kk)];
-        const f2 B = bufA[pidx(kk == 0 ? 0 : kP - kk)];
-        const f2 sm = add_cj(A, B), df = sub_cj(A, B);
-        const f2 wd = cmul(rec_post ? pw_k : a.post[kk], df);
+        const f2 wk = rec_post ? pw_k : a.post[kk];
         pw_k = cmul(pw_k, pstep);
-        const f2 X = add_mi(sm, wd);
-        const f2 q = X * X;
-        const float pw = (q.x + q.y) * qscale.x + 1e-12f;
-        out[i] = kDb * __builtin_amdgcn_logf(pw);
-      }
-    }
-    // slide the window: pairs r >= 4 become r - 4, the prefetched pairs fill r = 4..7
-    if (more) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        raw[r] = raw[r + 4];
-        raw[r + 4] = nx[r];
+        for (int q = 0; q < nfr; ++q) {
+          const f2 A = lds_ld(&buf[q][pidx(kk == kP ? 0 : kk)]);
+          const f2 B = lds_ld(&buf[q][pidx(kk == 0 ? 0 : kP - kk)]);
+          const f2 sm = add_cj(A, B), df = sub_cj(A, B);
+          const f2 wd = cmul(wk, df);
+          const f2 X = add_mi(sm, wd);
+          const f2 qq = X * X;
+          const float pw = (qq.x + qq.y) * qscale.x + 1e-12f;
+          a.out[((int64_t)slot * a.nt_out + f + q) * a.nf_out + i] = kDb * __builtin_amdgcn_logf(pw);
+        }
       }
     }
   }

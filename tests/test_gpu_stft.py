@@ -69,3 +69,22 @@ def test_any_fft_length_matches_scipy(gpu, oracle, fs, bpt, sps, cplx, dt, metho
     tight, loose = (1e-3, 0.25) if ref.dtype == np.float32 else (1e-6, 1e-3)
     assert d[strong].max() <= tight, d[strong].max()
     assert d.max() <= loose, d.max()
+
+
+@pytest.mark.parametrize("frames", [1, 2, 3, 5, 6, 7, 11, 13])
+def test_production_stft_ragged_frame_counts(gpu, oracle, frames):
+    """k_stft3840p transforms two frames per pass in runs of 6: runs that end on an odd frame (the
+    second frame of the last pass absent) and runs shorter than a chunk match scipy like full ones."""
+    from ft8_demodulator_amd import _lib, calculate_spectrogram
+    fs, n = 12000, (frames - 1) * 960 + 1920
+    ctx = _lib.context()
+    assert _lib.lib().ft8_stft_method(ctx.handle, fs, 2, 2, n, _lib.FT8_F32) == P38
+    rng = np.random.default_rng(frames)
+    x = (rng.normal(size=n) + 3 * np.cos(2 * np.pi * 1234.5 * np.arange(n) / fs)).astype(np.float32)
+    spec, f, t = calculate_spectrogram(x, fs, 2, 2)
+    ref, fr, tr = oracle.calculate_spectrogram(x, fs, 2, 2)
+    assert spec.shape == ref.shape and t.size in spec.shape  # frame counts of both parities across the cases
+    strong = ref >= (ref.max(axis=0, keepdims=True) - 60.0)
+    d = np.abs(spec.astype(np.float64) - ref.astype(np.float64))
+    assert d[strong].max() <= 1e-3, d[strong].max()
+    assert d.max() <= 0.25, d.max()
