@@ -233,8 +233,9 @@ def subtract_redecode(dev, n_slots=334, signals=50, iters=50, reps=3):
             "true_decodes_per_slot_pass1": true1 / n_slots, "true_decodes_per_slot_pass2": true2 / n_slots,
             "false_decodes": int(false),
             "stages_ms": {k: v[0] / reps for k, v in tm.items() if v[1] > 0},
-            "data": "synthetic (ft8_demodulator_amd.synth, seeds 200000..), parity unpinned: the reference "
-                    "has no second pass"}
+            "data": "synthetic (ft8_demodulator_amd.synth, seeds 200000..); the reference has no second pass: "
+                    "pass 2 is pinned against the CPU restatement oracle/subtract.py "
+                    "(tests/test_gpu_subtract_oracle.py)"}
 
 
 DRIFT_PARAMS = {"bins_per_tone": 2, "steps_per_symbol": 8}  # the reference test's correction params
