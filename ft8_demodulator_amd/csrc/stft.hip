@@ -323,12 +323,17 @@ __device__ __forceinline__ CT db_of(CT v) {
 // dB values the same way; closer ones (and NaN) compare their dB values exactly, first index on
 // ties.  Every decision equals the comparison of the (dB, -index) keys, so any reduction tree
 // returns np.argmax of the dB row while taking a log only for near ties.
+// Equal levels have equal dB values, so the first index wins without a log (every bin of an
+// all-zero frame, e.g. the beacon test's pads).  The log path stays inlined: as a call
+// (__noinline__) it cost the float64 drift STFT 10 % (11.5 -> 12.6 ms per 256-signal launch,
+// profiles/r3_drift_stft_ab.log).
 template <typename CT>
 __device__ __forceinline__ bool level_better(CT la, int ia, CT lb, int ib) {
   constexpr CT eps = sizeof(CT) == 4 ? (CT)1e-4 : (CT)1e-9;
   if (la == la && lb == lb) {
     if (la > lb * ((CT)1 + eps)) return true;
     if (lb > la * ((CT)1 + eps)) return false;
+    if (la == lb) return ia < ib;
   }
   return argmax_better(db_of(la), ia, db_of(lb), ib);
 }
@@ -470,7 +475,9 @@ __device__ __forceinline__ cplx<CT> load_c(const InT* x, int64_t n) {
   }
 }
 
-template <typename InT, typename CT, int M>
+// AMAX: the argmax epilogue (its own instantiation: a kernel carrying both epilogues is allocated
+// for the dB one's fifteen inlined float64 log10)
+template <typename InT, typename CT, int M, bool AMAX>
 __global__ __launch_bounds__(kC38Threads, 2) void k_stftc3840(StftArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   cplx<CT>* buf = reinterpret_cast<cplx<CT>*>(smem);
@@ -489,6 +496,7 @@ __global__ __launch_bounds__(kC38Threads, 2) void k_stftc3840(StftArgs a) {
   const CT* win = reinterpret_cast<const CT*>(a.window);
   const bool s1 = t < 240;
   for (int n = t; n < 1920; n += kC38Threads) wl[n] = win[n];
+  __syncthreads();  // stage 1 reads other threads' window entries
   // twiddle seeds: stage 2 W_256^k = W_3840^(15 k) (k = t % 16), stage 3 W_3840^t; their powers are
   // formed by complex recurrence each frame (relative error ~15 ulp, far inside the tolerances)
   cplx<CT> s2 = tw[15 * (t & 15)], s3 = tw[t];
@@ -500,7 +508,7 @@ __global__ __launch_bounds__(kC38Threads, 2) void k_stftc3840(StftArgs a) {
     for (int r = 0; r < 8; ++r) raw[r] = s1 ? load_c<InT, CT>(xs, base + t + 240 * r) : cplx<CT>{(CT)0, (CT)0};
   }
   const CT scale = (CT)a.scale;
-  const bool amax = a.argmax != nullptr;
+  constexpr bool amax = AMAX;
   const int k_lo = a.f_lo, k_hi = a.f_lo + a.nf_out;
   for (int f = f_begin; f < f_end; ++f) {
     // re-opaque the seeds so the per-frame twiddle powers are not hoisted into ~60 live registers
@@ -566,7 +574,7 @@ __global__ __launch_bounds__(kC38Threads, 2) void k_stftc3840(StftArgs a) {
     CT lv[15];
 #pragma unroll
     for (int r = 0; r < 15; ++r) lv[r] = (CT)1e-12 + (v[r].x * v[r].x + v[r].y * v[r].y) * scale;
-    if (!amax) {
+    if constexpr (!amax) {
       CT* out = reinterpret_cast<CT*>(a.out) + ((int64_t)slot * nt + f) * a.nf_out;
 #pragma unroll
       for (int r = 0; r < 15; ++r) {
@@ -624,12 +632,16 @@ hipError_t launch_c3840(const StftLaunch& L, StftArgs a, hipStream_t s) {
     hipLaunchKernelGGL(kern, grid, dim3(kC38Threads), lds, s, a);
     return hipGetLastError();
   };
-  switch (L.hop) {
-    case 240: return go(k_stftc3840<InT, CT, 1>);
-    case 480: return go(k_stftc3840<InT, CT, 2>);
-    case 960: return go(k_stftc3840<InT, CT, 4>);
-    default: return go(k_stftc3840<InT, CT, 8>);
-  }
+  auto go_m = [&](auto am) {
+    constexpr bool AM = decltype(am)::value;
+    switch (L.hop) {
+      case 240: return go(k_stftc3840<InT, CT, 1, AM>);
+      case 480: return go(k_stftc3840<InT, CT, 2, AM>);
+      case 960: return go(k_stftc3840<InT, CT, 4, AM>);
+      default: return go(k_stftc3840<InT, CT, 8, AM>);
+    }
+  };
+  return a.argmax != nullptr ? go_m(std::true_type{}) : go_m(std::false_type{});
 }
 
 // ---- k_stft_dft: direct DFT for lengths the FFT plans cannot take ---------------------------
