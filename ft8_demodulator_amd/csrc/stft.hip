@@ -323,17 +323,15 @@ __device__ __forceinline__ CT db_of(CT v) {
 // dB values the same way; closer ones (and NaN) compare their dB values exactly, first index on
 // ties.  Every decision equals the comparison of the (dB, -index) keys, so any reduction tree
 // returns np.argmax of the dB row while taking a log only for near ties.
-// Equal levels have equal dB values, so the first index wins without a log (every bin of an
-// all-zero frame, e.g. the beacon test's pads).  The log path stays inlined: as a call
-// (__noinline__) it cost the float64 drift STFT 10 % (11.5 -> 12.6 ms per 256-signal launch,
-// profiles/r3_drift_stft_ab.log).
+// (Measured and not kept in round 3, profiles/r3_drift_stft_ab.log: the log path as a call
+// (__noinline__), 11.5 -> 12.6 ms per float64 drift call; an early first-index return for exactly
+// equal levels, 12.9 ms -- each changed the code generation of the inlined comparison sites.)
 template <typename CT>
 __device__ __forceinline__ bool level_better(CT la, int ia, CT lb, int ib) {
   constexpr CT eps = sizeof(CT) == 4 ? (CT)1e-4 : (CT)1e-9;
   if (la == la && lb == lb) {
     if (la > lb * ((CT)1 + eps)) return true;
     if (lb > la * ((CT)1 + eps)) return false;
-    if (la == lb) return ia < ib;
   }
   return argmax_better(db_of(la), ia, db_of(lb), ib);
 }

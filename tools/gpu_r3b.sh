@@ -1,10 +1,13 @@
-# Round-3 GPU pass B: gpu tests, smoke, PMC passes (build-stamped summaries), the default bench line,
-# and a rocprofv3 kernel trace of the headline workload.  usage: bash tools/gpu_r3b.sh TAG
+# Round-3 GPU pass B: gpu tests, smoke, PMC passes (build-stamped summaries, placed in the box's
+# profiles/ so the bench line reads this build's counters), the default bench line, and a rocprofv3
+# kernel trace of the headline workload.  usage: bash tools/gpu_r3b.sh TAG  (then copy
+# gpurun_out/TAG_pmc*.json into profiles/ here)
 set -o pipefail
 T=${1:-r3}
 mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest tests -x -v -rP --timeout 300 --timeout-method thread -m gpu > gpurun_out/${T}_tests.log 2>&1 &&
 timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${T}_smoke.log 2>&1 &&
 bash tools/gpu_pmc_r3.sh ${T} &&
-cd $GRAFT_REPO_ROOT && timeout -k 10 600 python -u bench.py > gpurun_out/${T}_bench.log 2> gpurun_out/${T}_bench.err &&
+cd $GRAFT_REPO_ROOT && cp gpurun_out/${T}_pmc.json gpurun_out/${T}_pmc2.json gpurun_out/${T}_pmc_traffic.json profiles/ &&
+timeout -k 10 600 python -u bench.py > gpurun_out/${T}_bench.log 2> gpurun_out/${T}_bench.err &&
 bash tools/gpu_prof.sh ${T}
