@@ -1,0 +1,61 @@
+"""bench.py's host-side helpers (CPU): the algorithmic FLOP count behind roofline.achieved, the
+build-matched counter lookup behind roofline.traffic / issue, the parity summary, the core count."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+
+@pytest.fixture(scope="module")
+def bench():
+    import importlib.util
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(root, "bench.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def test_bp_flops_per_sweep(bench):
+    # 15 306 FP64 flops per message-passing sweep (ldpc_decoder.py:88-108)
+    assert bench.bp_flops_per_pass() == 15306
+
+
+def test_counters_for_build_matches_the_running_build(bench, tmp_path, monkeypatch):
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    files = {"r2_v17_pmc.json": "B", "r3_v2_pmc.json": "A", "r3_v10_pmc.json": "B", "r3_v9_pmc.json": "C"}
+    for name, bid in files.items():
+        (prof / name).write_text(json.dumps({"build_id": bid, "kernels": {"k_bp": {"src": name}}}))
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    k, src = bench.counters_for_build("r*_v*_pmc.json", "B")
+    assert src == os.path.join("profiles", "r3_v10_pmc.json") and k["k_bp"]["src"] == "r3_v10_pmc.json"
+    k, src = bench.counters_for_build("r*_v*_pmc.json", "A")
+    assert src == os.path.join("profiles", "r3_v2_pmc.json")
+    k, src = bench.counters_for_build("r*_v*_pmc.json", "Z")   # no summary of this build: flagged stale
+    assert k is None and src.startswith("stale: profiles/r3_v10_pmc.json (build B)")
+    assert bench.counters_for_build("r*_v*_nothing.json", "B") == (None, None)
+
+
+def test_parity_summary(bench):
+    dt = np.dtype([("payload", "u1", (10,)), ("crc_calculated", "<u2"), ("abs_time", "<i4"),
+                   ("abs_freq", "<i4"), ("score", "<f4")])
+    g = np.zeros(2, dt)
+    g["payload"][0, 0], g["payload"][1, 0] = 1, 2
+    g["crc_calculated"] = [7, 9]
+    g["abs_time"] = [960, 1920]
+    g["abs_freq"] = [100, 200]
+    g["score"] = [3.5, 4.0]
+    cpu = [(bytes(r["payload"]).hex(), int(r["crc_calculated"]), int(r["abs_time"]) / 12000,
+            (int(r["abs_freq"]) / 2) * 6.25, float(r["score"]) + 1e-6) for r in g]
+    p = bench.parity_check([g], [cpu])
+    assert p["payload_crc_multiset_equal"] and p["ordered_lists_equal_slots"] == 1
+    assert 0 < p["max_abs_score_diff"] < 1e-5
+    p = bench.parity_check([g], [cpu[:1]])
+    assert p["mismatching_slots"] == [0] and p["decodes_gpu"] == 2 and p["decodes_cpu"] == 1
+
+
+def test_host_cores(bench):
+    n, basis = bench.host_cores()
+    assert n >= 1 and "sched_getaffinity" in basis
