@@ -266,3 +266,27 @@ def test_packed_records_on_device(gpu):
     assert int(small[:8].cpu().view(torch.int64)) == len(want) and len(rows) == 3
     assert rows.tobytes() == want[:3].tobytes()
     assert over[: total - 3].cpu().numpy().tobytes() == want[3:].tobytes()
+
+
+@pytest.mark.parametrize("band", [(800.0, 2300.0), (0.0, 1500.0), (2000.0, None)])
+def test_band_limited_production_geometry_matches_oracle(gpu, oracle, band):
+    """12 kHz slots decoded with freq_min / freq_max: the production STFT's band-limited epilogue
+    (kept bins f_lo .. f_lo + nf_out of the 3840-point real FFT, post-twiddles by recurrence) and
+    the narrowed candidate grid decode exactly what the oracle decodes with the same band; time
+    limits too."""
+    from ft8_demodulator_amd import decode_ft8_message, synth
+    x, _ = synth.make_slots(3, 40, seed=4242, device="cpu")
+    kw = dict(max_candidates=200, min_score=2, max_iterations=20, freq_min=band[0], freq_max=band[1])
+    if band[1] is None:
+        kw.update(time_min=1.0, time_max=12.0)
+    n_dec = 0
+    for s in range(x.shape[0]):
+        xs = x[s].numpy()
+        got = decode_ft8_message(xs, 12000, **kw)
+        ref = oracle.decode_ft8_message(xs, 12000, **kw)
+        n_dec += len(ref)
+        assert sorted((m.payload.hex(), m.hash, t, f) for m, _s, t, f, _sc in got) == \
+            sorted((p.hex(), h, t, f) for (p, h, _e, _ce, _cc, t, f, _sc) in ref), (band, s)
+        for (m, _s, t, f, sc), r in zip(sorted(got, key=lambda g: (g[2], g[3])), sorted(ref, key=lambda r: (r[5], r[6]))):
+            assert abs(float(sc) - float(r[7])) <= 1e-4
+    assert n_dec >= 3
