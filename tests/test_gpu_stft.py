@@ -45,6 +45,9 @@ ST, P38, CZ, DFT = 0, 1, 2, 3  # ft8_stft_method: Stockham, packed 3840, chirp-z
     (12000, 10, 10, False, np.float32, ST),  # nfft 19200: the 40-values-per-thread LDS FFT (P 9600)
     (12000, 5, 2, True, np.complex64, ST),   # complex nfft 9600 in (8192, 10240]: the same variant
     (12000, 2, 2, False, np.float32, P38),   # the production geometry
+    (12000, 2, 2, True, np.complex64, ST),   # complex input, nfft 3840: k_stftc3840 dB epilogue (hop 960)
+    (12000, 2, 8, True, np.complex64, ST),   # ... hop 240 (the beacon receiver's geometry), float32
+    (12000, 2, 8, True, np.complex128, ST),  # ... float64
 ])
 def test_any_fft_length_matches_scipy(gpu, oracle, fs, bpt, sps, cplx, dt, method):
     """Lengths without a 2/3/5/7 factorisation (or odd real nfft) take the chirp-z transform (or the
