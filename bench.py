@@ -153,7 +153,69 @@ def parity_check(gpu_recs, cpu_decodes, bpt=2):
                     "tests/test_gpu_bench_parity.py checks every slot of this batch stage by stage"}
 
 
-def bp_stress(ctx, dev, n=100000, iters=50, reps=3, sigma=0.85):
+def gather_check(flat, counts, totals, S, world, decoded, cap):
+    """The resolved all-gather of one step (N > 1) against the decode count all ranks reported:
+    rank r's records are its totals[r] rows, their slot ids lie in [r S, (r + 1) S) in nondecreasing
+    order, each global slot appears exactly counts[r][slot] times (capped counts), and the totals
+    add up to the all-reduced decode count.  flat: structured ft8_result array, rank-major."""
+    import numpy as np
+    tot = [int(t) for t in totals]
+    cnt = np.minimum(np.asarray(counts)[:, :S].astype(np.int64), cap)
+    slots = np.asarray(flat["slot"], dtype=np.int64)
+    per_slot = np.bincount(slots, minlength=world * S) if len(slots) else np.zeros(world * S, np.int64)
+    ok_range = bool(len(slots) == 0 or (slots.min() >= 0 and slots.max() < world * S))
+    ok_order = bool(np.all(np.diff(slots) >= 0)) if len(slots) else True
+    ok_counts = ok_range and per_slot.shape[0] == world * S and bool(np.array_equal(per_slot, cnt.reshape(-1)))
+    ok_rank = True
+    off = 0
+    for r in range(world):
+        seg = slots[off:off + tot[r]]
+        ok_rank &= bool(len(seg) == 0 or (seg.min() >= r * S and seg.max() < (r + 1) * S))
+        off += tot[r]
+    ok_total = sum(tot) == int(decoded) == len(slots) == int(cnt.sum())
+    return {"gather_ok": bool(ok_range and ok_order and ok_counts and ok_rank and ok_total),
+            "records": len(slots), "sum_totals": sum(tot), "decodes_all_reduced": int(decoded),
+            "slot_ids_in_range": ok_range, "slot_order": ok_order, "per_slot_counts_match": bool(ok_counts),
+            "rank_ranges": bool(ok_rank)}
+
+
+def shard_sample(flat, lo, m):
+    """The gathered records of global slots [lo, lo + m) -> per-slot lists (as SlotDecoder.records)."""
+    sl = flat["slot"]
+    return [flat[sl == lo + i] for i in range(m)]
+
+
+def bp_parity(llr, x, plain, res, iters, n_sample):
+    """bp_stress's launch vs the oracle (oracle/ft8_oracle.c, pinned to the reference's bp_decode)
+    on n_sample evenly spaced vectors: normalised LLRs, hard decisions and min_errors bit-exact,
+    CRC status and payload of every vector equal to the oracle's decode tail."""
+    import numpy as np
+    from ft8_demodulator_amd import _lib
+    from oracle import oracle as O
+    n = llr.shape[0]
+    idx = np.unique(np.linspace(0, n - 1, min(n_sample, n)).astype(np.int64))
+    xs = x[idx].cpu().numpy()
+    ps = plain[idx].cpu().numpy()
+    rec = res.view(-1, _lib.RESULT_DTYPE.itemsize)[idx].cpu().numpy().reshape(-1).view(_lib.RESULT_DTYPE)
+    t0 = time.perf_counter()
+    bad_norm, bad_bp, bad_tail = [], [], []
+    for j, i in enumerate(idx):
+        xr = O.normalize(llr[i])
+        if not np.array_equal(xs[j].view(np.uint64), xr.view(np.uint64)):
+            bad_norm.append(int(i))
+        pr, er = O.bp_decode(xr, iters)
+        if er != int(rec[j]["ldpc_errors"]) or not np.array_equal(pr, ps[j]):
+            bad_bp.append(int(i))
+        ok, pay, _ce, cc = O.decode_tail(pr, er)
+        if bool(rec[j]["ok"]) != ok or int(rec[j]["crc_calculated"]) != cc or (ok and bytes(rec[j]["payload"]) != pay):
+            bad_tail.append(int(i))
+    return {"vectors": int(len(idx)), "sample": f"every {n // max(len(idx), 1)}th of the {n} launch vectors",
+            "normalize_bit_exact": not bad_norm, "bp_bit_exact": not bad_bp, "crc_payload_equal": not bad_tail,
+            "mismatches": {"normalize": bad_norm[:10], "bp": bad_bp[:10], "tail": bad_tail[:10]},
+            "oracle_s": time.perf_counter() - t0, "oracle": "oracle/ft8_oracle.c (bp_decode, ldpc_decoder.py:54-113)"}
+
+
+def bp_stress(ctx, dev, n=100000, iters=50, reps=3, sigma=0.85, n_sample=2000):
     """BASELINE config 4 (first pass): n LLR vectors from codewords of random payloads,
     (2b-1) + sigma N(0,1), ftx_normalize_logl on the device, then ft8_bp with `iters` iterations.
     Returns candidates/s and the k_bp roofline for this launch shape."""
@@ -183,16 +245,62 @@ def bp_stress(ctx, dev, n=100000, iters=50, reps=3, sigma=0.85):
     bp_ms = dt / reps * 1e3  # one k_bp launch (+ its 4-byte counter reset) per call, back to back
     flops = (cn["passes"] * bp_flops_per_pass() + cn["iterations"] * 174 * 3) / reps
     tf = flops / (bp_ms * 1e-3) / 1e12
+    # parity of this very launch shape, after the timing: the same call once more with the hard
+    # decisions written out, and an evenly spaced sample checked against the oracle
+    plain = torch.empty((n, 174), dtype=torch.uint8, device=dev)
+    ctx.check(L.ft8_bp(ctx.handle, _lib.ptr(x), n, iters, _lib.ptr(plain), _lib.ptr(res), st), "ft8_bp")
+    torch.cuda.synchronize()
+    parity = bp_parity(llr, x, plain, res, iters, n_sample)
     return {"workload": f"BASELINE config 4 first pass: {n} LLR vectors (codewords of random payloads, "
                         f"(2b-1)+{sigma}*N(0,1), normalised), {iters} BP iterations",
             "candidates_per_s": n * reps / dt, "ms_per_launch": bp_ms, "timing": "wall clock over back-to-back launches",
             "converged_frac": cn["converged"] / max(cn["candidates"], 1),
             "sweeps_per_launch": cn["passes"] / reps,
             "roofline": {"kernel": "k_bp", "bound": "fp64-valu", "achieved": tf, "peak": FP64_VECTOR_PEAK_TFLOPS,
-                         "unit": "TFLOP/s", "frac": tf / FP64_VECTOR_PEAK_TFLOPS}}
+                         "unit": "TFLOP/s", "frac": tf / FP64_VECTOR_PEAK_TFLOPS},
+            "parity": parity}
 
 
-def subtract_redecode(dev, n_slots=334, signals=50, iters=50, reps=3):
+SUB_SEED0 = 200000
+
+
+def subtract_oracle_worker(args):
+    """One slot of the subtract leg through oracle/subtract.py (CPU, float64 NumPy restatement of
+    FT8_FLAG_SUBTRACT): the slot synthesised on the CPU, top-k pass 1, a fit per decode (record order
+    = the selection's order), the residual, top-k pass 2 -> (samples, pass-1 payloads, new payloads)."""
+    import numpy as np
+    from ft8_demodulator_amd import synth
+    from oracle import subtract as OS
+    from ft8_demodulator_amd._pipeline import make_plan
+    seed, signals, iters = args
+    x, _ = synth.make_slots(1, signals, fs=12000, snr_db=(-24.0, -10.0), seeds=[seed], device="cpu")
+    xs = x[0].numpy()
+    plan = make_plan(xs.shape[0], 12000)
+    d1 = OS.decode_topk(xs, 12000, 300, 2, iters)
+    recs = np.zeros(len(d1), dtype=[("payload", "u1", 10), ("ok", "u1"), ("abs_time", "<i4"), ("abs_freq", "<i4")])
+    for i, (pay, at, af) in enumerate(d1):
+        recs[i] = (np.frombuffer(pay, np.uint8), 1, at, af)
+    ofit = OS.fits(xs, recs, 12000, plan.nperseg, plan.hop, plan.nfft, plan.t_lo, plan.f_lo)
+    res = OS.residual(xs, ofit, plan.nperseg, 12000).astype(np.float32)
+    p1 = {pay for pay, _, _ in d1}
+    new = {pay for pay, _, _ in OS.decode_topk(res, 12000, 300, 2, iters)} - p1
+    return xs, sorted(p.hex() for p in p1), sorted(p.hex() for p in new), sum(f is not None for f in ofit)
+
+
+def subtract_oracle(n, procs, signals=50, iters=50):
+    """The first n slots of the subtract leg through oracle/subtract.py, `procs` processes, before
+    the GPU is touched -> (samples [n, N] float32, per-slot (pass-1, new) payload hex lists, info)."""
+    import multiprocessing as mp
+    import numpy as np
+    ctx = mp.get_context("fork")
+    t0 = time.perf_counter()
+    with ctx.Pool(min(procs, n), initializer=_worker_init) as pool:
+        out = pool.map(subtract_oracle_worker, [(SUB_SEED0 + b, signals, iters) for b in range(n)], chunksize=1)
+    return (np.stack([o[0] for o in out]), [(o[1], o[2]) for o in out],
+            {"fits": sum(o[3] for o in out), "oracle_wall_s": time.perf_counter() - t0})
+
+
+def subtract_redecode(dev, n_slots=334, signals=50, iters=50, reps=3, oracle_sample=None):
     """BASELINE config 4 with the subtract-and-redecode second pass (build-defined):
     334 crowded slots x K=300 candidates = 100 200 LDPC candidates per pass, 50 BP iterations,
     top-k candidate selection (FT8_FLAG_TOPK) and FT8_FLAG_SUBTRACT: pass 1, fit + subtract every
@@ -201,7 +309,12 @@ def subtract_redecode(dev, n_slots=334, signals=50, iters=50, reps=3):
     import torch
     from ft8_demodulator_amd import _lib, synth
     from ft8_demodulator_amd._pipeline import SlotDecoder
-    x, truths = synth.make_slots(n_slots, signals, fs=12000, snr_db=(-24.0, -10.0), seed=200000, device=dev)
+    x, truths = synth.make_slots(n_slots, signals, fs=12000, snr_db=(-24.0, -10.0), seed=SUB_SEED0, device=dev)
+    n_or = 0
+    if oracle_sample is not None:
+        # the oracle's slots were synthesised on the CPU: decode those very bytes
+        n_or = oracle_sample[0].shape[0]
+        x[:n_or] = torch.from_numpy(oracle_sample[0]).to(dev)
     dec = SlotDecoder(12000, 2, 2, max_candidates=300, min_score=2, max_iterations=iters, device=dev,
                       flags=_lib.FT8_FLAG_TOPK | _lib.FT8_FLAG_SUBTRACT)
     recs = dec.records(x, _lib.FT8_F32)
@@ -211,6 +324,25 @@ def subtract_redecode(dev, n_slots=334, signals=50, iters=50, reps=3):
         g1 = set(bytes(r["payload"]) for r in recs[s] if r["pass_index"] == 0)
         g2 = set(bytes(r["payload"]) for r in recs[s] if r["pass_index"] == 1)
         true1, true2, false = true1 + len(g1 & tr), true2 + len(g2 & tr), false + len((g1 | g2) - tr)
+    parity = None
+    if n_or:
+        mism1, mism2, n1, n2 = [], [], 0, 0
+        for s_ in range(n_or):
+            g1 = sorted(bytes(r["payload"]).hex() for r in recs[s_] if r["pass_index"] == 0)
+            g2 = sorted(bytes(r["payload"]).hex() for r in recs[s_] if r["pass_index"] == 1)
+            o1, o2 = oracle_sample[1][s_]
+            n1, n2 = n1 + len(o1), n2 + len(o2)
+            if g1 != o1:
+                mism1.append(s_)
+            if g2 != o2:
+                mism2.append(s_)
+        parity = {"slots": n_or, "oracle_pass1_decodes": n1, "oracle_pass2_new_decodes": n2,
+                  "oracle_fits": oracle_sample[2]["fits"], "oracle_wall_s": oracle_sample[2]["oracle_wall_s"],
+                  "pass1_payloads_equal": not mism1, "pass2_new_payloads_equal": not mism2,
+                  "mismatching_slots_pass1": mism1, "mismatching_slots_pass2": mism2,
+                  "oracle": "oracle/subtract.py (CPU float64 restatement of the build-defined second pass; the "
+                            "reference has no second pass, so pass 2 is pinned to the restatement, not the reference)",
+                  "from": "the first slots of this leg's batch, synthesised on the CPU and uploaded (same bytes)"}
     ctx = dec.ctx
     torch.cuda.synchronize()
     ctx.set_timing(True)
@@ -232,6 +364,7 @@ def subtract_redecode(dev, n_slots=334, signals=50, iters=50, reps=3):
             "slots_per_s": n_slots * reps / dt, "ms_per_launch": dt / reps * 1e3,
             "true_decodes_per_slot_pass1": true1 / n_slots, "true_decodes_per_slot_pass2": true2 / n_slots,
             "false_decodes": int(false),
+            "parity": parity,
             "stages_ms": {k: v[0] / reps for k, v in tm.items() if v[1] > 0},
             "data": "synthetic (ft8_demodulator_amd.synth, seeds 200000..); the reference has no second pass: "
                     "pass 2 is pinned against the CPU restatement oracle/subtract.py "
@@ -566,10 +699,15 @@ def main():
     ap.add_argument("--signals", type=int, default=50)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-slots", type=int, default=256)
+    ap.add_argument("--shard-parity-slots", type=int, default=32,
+                    help="N > 1: slots of each rank's shard decoded by the oracle before the GPU is touched and "
+                         "compared with the gathered records of the last timed step")
     ap.add_argument("--stage-steps", type=int, default=10, help="steps per single-stage event pass")
     ap.add_argument("--no-bp-stress", action="store_true", help="skip the config-4 BP stress leg")
     ap.add_argument("--no-h2d", action="store_true", help="skip the PCIe-inclusive streaming leg")
     ap.add_argument("--no-subtract", action="store_true", help="skip the config-4 subtract-and-redecode leg")
+    ap.add_argument("--subtract-oracle-slots", type=int, default=8,
+                    help="slots of the subtract leg checked against oracle/subtract.py (0: none)")
     ap.add_argument("--no-drift", action="store_true", help="skip the frequency-drift correction leg")
     ap.add_argument("--gather", action="store_true",
                     help="N = 1: every timed step also packs its decodes and all-gathers them over a world-size-1 "
@@ -604,11 +742,27 @@ def main():
     seed0 = 100000 + rank * S  # global slot g uses seed 100000 + g
     cpu = drift_cpu_port = None
     cpu_x = cpu_dec = None
+    shard_sample_wall = None
     if rank == 0 and world == 1 and not args.no_cpu and args.cpu_slots > 0:
         procs, basis = host_cores()
         cpu, cpu_x, cpu_dec = cpu_baseline(kw, min(args.cpu_slots, S), procs, basis, seed0, args.signals)
         if not args.no_drift:
             drift_cpu_port = drift_cpu_baseline(procs)
+    sub_oracle = None
+    if rank == 0 and world == 1 and not args.no_cpu and not args.no_subtract and args.subtract_oracle_slots > 0:
+        sub_oracle = subtract_oracle(args.subtract_oracle_slots, host_cores()[0])
+    if False:
+        pass
+    elif world > 1 and args.shard_parity_slots > 0:
+        # every rank: the oracle decodes the first slots of this rank's own shard (global seeds
+        # 100000 + g) on its share of the host cores, before the GPU is touched; those bytes are
+        # the first rows of the rank's batch, so the gathered records of the last timed step are
+        # checked against them (gather.shard_parity)
+        procs, basis = host_cores()
+        procs = max(1, procs // world)
+        base_, cpu_x, cpu_dec = cpu_baseline(kw, min(args.shard_parity_slots, S), procs,
+                                             basis + f" // {world} ranks", seed0, args.signals)
+        shard_sample_wall = base_["wall_s"]
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
@@ -648,10 +802,12 @@ def main():
     gatherer = DecodeGatherer(S, dec.cap, slot_offset=rank * S) if exchange else None
     handles = []
 
-    def step():
+    def step(keep=False):
         out, counts = dec.run(x)
         if exchange:
-            handles[:] = [gatherer.start(out, counts)]
+            h = gatherer.start(out, counts)
+            if keep:
+                handles.append(h)   # every timed step's exchange is resolved after the loop
         return counts
 
     for _ in range(args.warmup):
@@ -662,18 +818,29 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        counts = step()
+        counts = step(keep=True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     decoded = int(counts.sum().item())
     gather = None
+    gather_last = None
     if exchange:
-        recs_g, _, totals_g = handles[0].resolve()   # collective: every rank resolves the last step's
+        from ft8_demodulator_amd.distributed import gathered_records, pack_bytes
+        rows_sent = gatherer.capacity
+        # resolve every timed step's exchange in issue order (collectives: all ranks do the same);
+        # a step whose total exceeded the capacity runs its overflow exchange here and grows it
+        over_steps = 0
+        for h in handles:
+            recs_g, cnts_g, totals_g = h.resolve()
+            over_steps += int(int(totals_g.max()) > h.capacity)
+        gather_last = (gathered_records(recs_g, totals_g), cnts_g.cpu().numpy(), totals_g.cpu().tolist())
+        handles.clear()
         gather = {"backend": dist.get_backend(), "world": world,
-                  "rows_per_rank_sent": gatherer.capacity, "bytes_per_rank_sent": 8 + 4 * S + gatherer.capacity * 40,
-                  "decodes_per_rank_last_step": totals_g.cpu().tolist(), "overflow_exchanges": gatherer.grown,
+                  "rows_per_rank_sent": rows_sent, "bytes_per_rank_sent": pack_bytes(gatherer.S_pad, rows_sent),
+                  "decodes_per_rank_last_step": gather_last[2], "steps_over_capacity": over_steps,
+                  "capacity_grown": gatherer.grown, "capacity_after": gatherer.capacity,
                   "host_sync_per_step": False}
 
     # per-kernel durations inside the real step sequence: one pass of `stage_steps` steps per stage,
@@ -715,8 +882,24 @@ def main():
         decoded = int(d.item())
 
     parity = None
-    if cpu_dec is not None:
+    if cpu_dec is not None and world == 1:
         parity = parity_check(dec.records(x[:n_cpu]), cpu_dec)
+    if gather is not None:
+        flat, cnts_np, tot_l = gather_last
+        gather.update(gather_check(flat, cnts_np, tot_l, S, world, decoded, dec.cap))
+        mine = None
+        if cpu_dec is not None:
+            # this rank's oracle sample against the gathered records of its global slots
+            mine = parity_check(shard_sample(flat, rank * S, n_cpu), cpu_dec)
+            mine = {"rank": rank, "global_slots": [rank * S, rank * S + n_cpu], "oracle_wall_s": shard_sample_wall,
+                    **{k: mine[k] for k in ("slots", "decodes_gpu", "decodes_cpu", "payload_crc_multiset_equal",
+                                            "mismatching_slots", "ordered_lists_equal_slots", "max_abs_score_diff")}}
+        per_rank = [mine]
+        if world > 1:
+            per_rank = [None] * world
+            dist.all_gather_object(per_rank, mine)
+        gather["shard_parity"] = per_rank
+        gather["shard_parity_ok"] = all(p_ is not None and p_["payload_crc_multiset_equal"] for p_ in per_rank)
 
     total_slots = S * world * args.steps
     value = total_slots / elapsed
@@ -753,7 +936,7 @@ def main():
         drift["rate_32768"] = drift_32k(dev)
     sub = None
     if world == 1 and not args.no_subtract:
-        sub = subtract_redecode(dev)
+        sub = subtract_redecode(dev, oracle_sample=sub_oracle)
 
     # HBM bytes and issue counters per launch from the committed rocprofv3 PMC summaries
     # (tools/pmc_traffic.py: FETCH_SIZE / WRITE_SIZE passes; tools/pmc_sq_json.py: the SQ pass), each

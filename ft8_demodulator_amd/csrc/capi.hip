@@ -361,7 +361,9 @@ int blue_tables(ft8_ctx* c, PlanEntry& e, int nfft, int L, int P, bool f64) {
 
 int get_plan(ft8_ctx* c, int nfft, bool cplx, bool f64, int nperseg, FftPlan* out) {
   for (auto& p : c->plans)
-    if (p.nfft == nfft && p.cplx == cplx && p.f64 == f64 && (!p.plan.blue || p.L == nperseg)) {
+    // a fallback plan (chirp-z or direct DFT) was chosen for one nperseg: the choice between the
+    // two depends on it, so such a plan is reused only for that nperseg
+    if (p.nfft == nfft && p.cplx == cplx && p.f64 == f64 && (!(p.plan.blue || p.plan.dft) || p.L == nperseg)) {
       *out = p.plan;
       return FT8_OK;
     }
@@ -398,6 +400,7 @@ int get_plan(ft8_ctx* c, int nfft, bool cplx, bool f64, int nperseg, FftPlan* ou
       P = nfft;
       e.plan.dft = 1;
       e.plan.nstages = 0;
+      e.L = nperseg;
     }
   }
   e.plan.P = P;
@@ -761,6 +764,7 @@ int subtract_core(ft8_ctx* c, const void* x, int dtype, float* resid, int64_t n_
   if (rc) return fail(c, rc, why);
   if (dtype != FT8_F32 && dtype != FT8_I16) return fail(c, FT8_E_UNSUPPORTED, "subtraction needs float32 or int16 samples");
   if (x_stride != r_stride) return fail(c, FT8_E_ARG, "residual and sample strides differ");
+  c->sub_slots = c->sub_cap = -1;  // no valid fits until this subtraction has been launched
   const int Q = sub_q(g.nperseg);
   if (Q == 0 || g.nperseg % g.hop != 0)
     return fail(c, FT8_E_UNSUPPORTED, "subtraction needs nsps with a divisor in [8, 32] and hop | nsps");
@@ -786,12 +790,13 @@ int subtract_core(ft8_ctx* c, const void* x, int dtype, float* resid, int64_t n_
   L.Pf = (const float*)c->gfsk_Pf.p;
   L.est = c->sub_est.p;
   L.Q = Q;
-  c->sub_slots = n_slots;
-  c->sub_cap = cap;
   StageTimer tm(c, 7, s);
   hipError_t e = launch_subtract(L, s);
   tm.done();
-  return e == hipSuccess ? FT8_OK : hipfail(c, e, "subtract launch");
+  if (e != hipSuccess) return hipfail(c, e, "subtract launch");
+  c->sub_slots = n_slots;
+  c->sub_cap = cap;
+  return FT8_OK;
 }
 
 // ---- frequency-drift correction ----------------------------------------------------------------
@@ -1233,7 +1238,12 @@ int ft8_subtract(ft8_ctx* c, const void* d_samples, int dtype, float* d_residual
                  void* stream) {
   if (c) c->replay_ok = false;
   if (!c || !p || n_slots < 0 || cap < 0 || n_samples < 0) return fail(c, FT8_E_ARG, "bad argument");
-  if (n_slots == 0 || n_samples == 0) return FT8_OK;
+  if (n_slots == 0 || n_samples == 0) {
+    // nothing to fit: an empty subtraction's (zero) fits are valid, a zero-length one's never written
+    c->sub_slots = n_slots == 0 ? 0 : -1;
+    c->sub_cap = n_slots == 0 ? cap : -1;
+    return FT8_OK;
+  }
   if (!d_samples || !d_residual || !d_counts || (cap > 0 && !d_res)) return fail(c, FT8_E_ARG, "null argument");
   if (slot_stride < n_samples && n_slots > 1) return fail(c, FT8_E_ARG, "slot_stride < n_samples");
   DeviceGuard dg(c->device);

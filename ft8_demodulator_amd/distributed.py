@@ -60,8 +60,12 @@ def pack_decodes_reference(records, counts, cap, capacity, slot_offset=0):
     S = counts.numel()
     c = counts.to(torch.int64).clamp(0, cap)
     total = int(c.sum())
-    rows = records[: S * cap * REC_BYTES].view(S, cap, REC_BYTES)
-    keep = torch.arange(cap, device=dev)[None, :] < c[:, None]
+    # a gatherer's padded slots (zero counts past this rank's records) hold no rows
+    S_rec = min(S, records.numel() // (cap * REC_BYTES)) if cap else 0
+    if int(c[S_rec:].sum()):
+        raise ValueError("counts name slots past the record buffer")
+    rows = records[: S_rec * cap * REC_BYTES].view(S_rec, cap, REC_BYTES)
+    keep = torch.arange(cap, device=dev)[None, :] < c[:S_rec, None]
     dense = rows[keep].clone()                                   # slot order, then candidate order
     if slot_offset and total:
         dense.view(torch.int32)[:, 2] += int(slot_offset)       # ft8_result.slot (bytes 8..11)
@@ -141,18 +145,44 @@ class GatherHandle:
 class DecodeGatherer:
     """All-gathers of a stream of batches (S slots per rank, `cap` records per slot): start() packs
     and issues the exchange without a host sync and returns a GatherHandle.  The capacity (rows per
-    rank) starts at `capacity` (default: 4 per slot, at least 64, at most S * cap) and grows to
-    1.25 x the largest total a resolved exchange reported beyond it."""
+    rank) starts at `capacity` (default: 4 per slot, at least 64, at most S_pad * cap) and grows to
+    1.25 x the largest total a resolved exchange reported beyond it.
 
-    def __init__(self, n_slots, cap, slot_offset=0, group=None, capacity=None):
+    all_gather_into_tensor needs the same buffer size on every rank, so the packed header is sized
+    for S_pad = the largest slot count of any rank (shard_range's shards differ by one): `max_slots`
+    when the caller knows it (ceil(n / world) for shard_range), else one all-reduce(MAX) of S at the
+    first start() (a host sync, once per gatherer).  A rank with fewer slots sends zero counts for
+    the missing ones; resolve() returns counts [world, S_pad], rank r's real slots first."""
+
+    def __init__(self, n_slots, cap, slot_offset=0, group=None, capacity=None, max_slots=None):
         self.S, self.cap, self.slot_offset, self.group = int(n_slots), int(cap), int(slot_offset), group
-        full = self.S * self.cap
-        self.capacity = min(full, int(capacity) if capacity is not None else max(64, 4 * self.S))
+        if max_slots is not None and int(max_slots) < self.S:
+            raise ValueError(f"max_slots {max_slots} < this rank's {self.S} slots")
+        self.S_pad = None if max_slots is None else int(max_slots)
+        self._capacity_arg = capacity
+        self.capacity = None
+        if self.S_pad is not None:
+            self._set_capacity()
         self.grown = 0
+
+    def _set_capacity(self):
+        full = self.S_pad * self.cap
+        c = self._capacity_arg
+        self.capacity = min(full, int(c) if c is not None else max(64, 4 * self.S_pad))
+
+    def _agree_slots(self, device):
+        """S_pad = max over ranks of S (one all-reduce; gloo on the host, RCCL on the device)."""
+        import torch
+        import torch.distributed as dist
+        dev = device if dist.get_backend(self.group) != "gloo" else torch.device("cpu")
+        t = torch.tensor([self.S], dtype=torch.int64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        self.S_pad = int(t.item())
+        self._set_capacity()
 
     def _grow(self, rows):
         if rows > self.capacity:
-            self.capacity = min(self.S * self.cap, (rows * 5 // 4 + 63) // 64 * 64)
+            self.capacity = min(self.S_pad * self.cap, (rows * 5 // 4 + 63) // 64 * 64)
             self.grown += 1
 
     def start(self, records, counts) -> GatherHandle:
@@ -160,21 +190,28 @@ class DecodeGatherer:
         import torch.distributed as dist
         if counts.numel() != self.S:
             raise ValueError(f"batch has {counts.numel()} slots, the gatherer {self.S}")
+        if self.S_pad is None:
+            self._agree_slots(records.device)
+        if self.S_pad > self.S:
+            pad = torch.zeros(self.S_pad, dtype=torch.int32, device=counts.device)
+            pad[: self.S] = counts.view(-1)
+            counts = pad
         send, over = pack_decodes(records, counts, self.cap, self.capacity, self.slot_offset)
         world = dist.get_world_size(self.group)
         out = torch.empty(world * send.numel(), dtype=torch.uint8, device=send.device)
         dist.all_gather_into_tensor(out, send, group=self.group)
-        return GatherHandle(out.view(world, -1), over, self.S, self.capacity, self.group, self._grow)
+        return GatherHandle(out.view(world, -1), over, self.S_pad, self.capacity, self.group, self._grow)
 
 
-def gather_decodes(records, counts, cap, capacity=None, group=None, slot_offset=0):
+def gather_decodes(records, counts, cap, capacity=None, group=None, slot_offset=0, max_slots=None):
     """One exchange of every rank's decodes, resolved at once (a host sync): packs this rank's
     records (capacity rows: the given number, or DecodeGatherer's default), all-gathers, and moves
     overflow rows in a second exchange if any rank exceeded the capacity -- so nothing is ever
     truncated.  slot_offset (this rank's first global slot, e.g. shard_range's lo) is added to every
-    record's slot.  -> (records uint8 [world, max(totals), 40], counts int32 [world, S], totals
-    int64 [world]); rank r's decodes are rows [0, totals[r])."""
-    g = DecodeGatherer(counts.numel(), cap, slot_offset, group, capacity)
+    record's slot.  Ranks may hold different slot counts (max_slots: the largest, or None to agree
+    on it by an all-reduce).  -> (records uint8 [world, max(totals), 40], counts int32 [world,
+    S_pad], totals int64 [world]); rank r's decodes are rows [0, totals[r])."""
+    g = DecodeGatherer(counts.numel(), cap, slot_offset, group, capacity, max_slots)
     return g.start(records, counts).resolve()
 
 

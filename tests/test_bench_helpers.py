@@ -59,3 +59,26 @@ def test_parity_summary(bench):
 def test_host_cores(bench):
     n, basis = bench.host_cores()
     assert n >= 1 and "sched_getaffinity" in basis
+
+
+def test_gather_check_and_shard_sample(bench):
+    """The N > 1 line's self-check of the gathered decodes (bench.gather_check) and the per-rank
+    sample lookup (bench.shard_sample) on a hand-made two-rank exchange."""
+    from ft8_demodulator_amd._lib import RESULT_DTYPE
+    S, world, cap = 3, 2, 4
+    counts = np.array([[1, 0, 2, 0], [0, 3, 1, 0]])          # S_pad 4: one zero pad column
+    slots = [0, 2, 2, 4, 4, 4, 5]
+    flat = np.zeros(len(slots), RESULT_DTYPE)
+    flat["slot"] = slots
+    flat["payload"][:, 0] = np.arange(len(slots))
+    ok = bench.gather_check(flat, counts, [3, 4], S, world, 7, cap)
+    assert ok["gather_ok"] and ok["records"] == 7
+    # a record under the wrong rank, a lost record, a wrong all-reduced count
+    bad = flat.copy()
+    bad["slot"][2] = 3
+    assert not bench.gather_check(bad, counts, [3, 4], S, world, 7, cap)["gather_ok"]
+    assert not bench.gather_check(flat[:-1], counts, [3, 3], S, world, 6, cap)["gather_ok"]
+    assert not bench.gather_check(flat, counts, [3, 4], S, world, 8, cap)["gather_ok"]
+    per = bench.shard_sample(flat, 3, 3)
+    assert [len(p) for p in per] == [0, 3, 1]
+    assert per[1]["payload"][:, 0].tolist() == [3, 4, 5]

@@ -93,3 +93,59 @@ def test_gloo_world2_gather():
         want = [(s, j) for s in range(8) for j in range(min(6 + s, 12))]
         assert list(zip(slots, rows)) == want
         assert tags == slots  # the global slot written into byte 0 agrees with the offset slot field
+
+
+def _uneven_worker(rank, world, port, n_slots, q):
+    """Shards of different sizes (shard_range of 7 slots over 2 ranks: 4 and 3): the packed buffers
+    must have one size on every rank, whether the gatherer learns the largest shard by an all-reduce
+    or is told it."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        try:
+            from ft8_demodulator_amd.distributed import (DecodeGatherer, gather_decodes, gathered_records,
+                                                          shard_range)
+            lo, hi = shard_range(n_slots, rank, world)
+            cap = 5
+            rec, cnt = _records(lo, hi, cap, torch.arange(lo, hi, dtype=torch.int32) % 4 + 1)
+            out = []
+            for kw in ({}, {"max_slots": -(-n_slots // world)}):
+                recs, cnts, tot = gather_decodes(rec, cnt, cap, capacity=3, slot_offset=lo, **kw)
+                flat = gathered_records(recs, tot)
+                out.append((cnts.tolist(), tot.tolist(), flat["slot"].tolist(), flat["payload"][:, 0].tolist()))
+            # a gatherer reused over steps: the agreement happens once
+            g = DecodeGatherer(hi - lo, cap, slot_offset=lo)
+            for _ in range(2):
+                r2, c2, t2 = g.start(rec, cnt).resolve()
+            out.append((g.S_pad, g.capacity, t2.tolist()))
+            q.put((rank, out))
+        except Exception as e:  # noqa: BLE001
+            q.put((rank, "error " + repr(e)))
+            raise
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_uneven_shards():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 31500 + (os.getpid() % 2000)
+    ps = [ctx.Process(target=_uneven_worker, args=(r, 2, port, 7, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    out = [q.get(timeout=120) for _ in ps]
+    assert all(not isinstance(o[1], str) for o in out), out
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # rank 0: slots 0..3 with counts 1,2,3,4 (10 rows); rank 1: slots 4..6 with counts 1,2,3 (+ a
+    # zero pad slot): 6 rows; capacity 3 -> both take the overflow exchange
+    want_slots = [s for s in range(7) for _ in range(s % 4 + 1)]
+    want_rows = [j for s in range(7) for j in range(s % 4 + 1)]
+    for rank, res in out:
+        for cnts, tot, slots, rows in res[:2]:
+            assert cnts == [[1, 2, 3, 4], [1, 2, 3, 0]]
+            assert tot == [10, 6]
+            assert slots == want_slots and rows == want_rows
+        assert res[2] == (4, 20, [10, 6])  # capacity min(S_pad * cap, max(64, 4 S_pad))
