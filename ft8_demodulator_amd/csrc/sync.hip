@@ -1013,11 +1013,244 @@ __global__ __launch_bounds__(kSelThreads) void k_topk(SelectArgs a) {
   }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// FT8_FLAG_TOPK from the compact score layout (k_score2 wrote only each segment's passing scores,
+// packed at the segment's start in column order, plus its column masks).  The passing scores of a
+// slot, numbered densely d = 0 .. total-1 in segment order, are in scan order (a row's segments
+// are its column ranges), so d serves as the scan-order tie key and the grid index of a selected
+// candidate is recovered from its segment's mask only for the N outputs.  One 1024-thread
+// workgroup per slot: segment offsets by a block scan of the mask popcounts; the passing scores
+// staged in LDS (a crowded 12 kHz slot holds ~12.5 k, 50 KB) -- or, past the LDS budget, read
+// from HBM by one wave per segment on every pass -- then k_topk's radix select, collection and
+// bitonic sort on LDS.  Round 3's k_topk read the full 670 KB grid of every slot per radix pass.
+// ---------------------------------------------------------------------------------------------
+constexpr int kTkcMaxSeg = 8192;     // segments per slot whose offsets live in LDS
+constexpr int kTkcRun = 16;          // staged values per thread and load batch
+
+__device__ __forceinline__ unsigned tk_key(float v) { return TkKey<float>::of(v); }
+
+// the segment holding dense index d: the last seg with off[seg] <= d (empty segments share their
+// successor's offset, so the last one is the non-empty one)
+__device__ __forceinline__ int tkc_seg(const int* off, int nsegs, int d) {
+  int lo = 0, hi = nsegs - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (off[mid] <= d) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
+__global__ __launch_bounds__(kSelThreads) void k_topkc(SelectArgs a, int M, int V) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int nsegs = a.NT * a.nseg;
+  unsigned* s_hist = reinterpret_cast<unsigned*>(smem);
+  int* s_off = reinterpret_cast<int*>(smem + kTkBins * sizeof(unsigned));
+  double* s_key = reinterpret_cast<double*>(s_off + ((nsegs + 2) & ~1));
+  int* s_sec = reinterpret_cast<int*>(s_key + M);
+  int* s_pay = s_sec + M;
+  float* s_val = reinterpret_cast<float*>(s_pay + M);
+  __shared__ int s_isum[kSelWaves + 1];
+  __shared__ unsigned s_prefix, s_mask;
+  __shared__ int s_need, s_done, s_eqcnt, s_cnt;
+
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid >> 6;
+  const int slot = blockIdx.x;  // == the XCD k_score2 wrote this slot's segments from (slot % 8)
+  const int64_t seg0 = (int64_t)slot * nsegs;
+  const uint64_t* mk = a.smask + 2 * seg0;
+  const float* sv = reinterpret_cast<const float*>(a.scores) + seg0 * kSegCols;
+  const int N = a.N;
+
+  // ---- segment offsets (dense index of each segment's first passing score)
+  int carry = 0;
+  for (int g0 = 0; g0 < nsegs; g0 += kSelThreads) {
+    const int sg = g0 + tid;
+    int c = 0;
+    if (sg < nsegs) c = __popcll(mk[2 * sg]) + __popcll(mk[2 * sg + 1]);
+    int ctot;
+    const int ex = block_excl_sum(c, s_isum, &ctot);
+    if (sg < nsegs) s_off[sg] = carry + ex;
+    carry += ctot;
+  }
+  const int total = carry;
+  if (tid == 0) {
+    s_off[nsegs] = total;
+    s_prefix = 0;
+    s_mask = 0;
+    s_need = N;
+    s_done = 0;
+    s_eqcnt = 0;
+    s_cnt = 0;
+  }
+  __syncthreads();
+  const bool staged = total <= V;
+  if (staged) {
+    // thread t copies the dense run [t per, (t + 1) per): one search, then a walk over segments;
+    // kTkcRun loads in flight
+    const int per = (total + kSelThreads - 1) / kSelThreads;
+    const int d_lo = min(total, tid * per), d_hi = min(total, d_lo + per);
+    if (d_lo < d_hi) {
+      int sg = tkc_seg(s_off, nsegs, d_lo);
+      for (int b = d_lo; b < d_hi; b += kTkcRun) {
+        int64_t src[kTkcRun];
+#pragma unroll
+        for (int u = 0; u < kTkcRun; ++u) {
+          const int d = b + u;
+          src[u] = -1;
+          if (d < d_hi) {
+            while (s_off[sg + 1] <= d) ++sg;
+            src[u] = (int64_t)sg * kSegCols + (d - s_off[sg]);
+          }
+        }
+        float v[kTkcRun];
+#pragma unroll
+        for (int u = 0; u < kTkcRun; ++u) v[u] = src[u] >= 0 ? sv[src[u]] : 0.0f;
+#pragma unroll
+        for (int u = 0; u < kTkcRun; ++u)
+          if (b + u < d_hi) s_val[b + u] = v[u];
+      }
+    }
+    __syncthreads();
+  }
+  // every passing score once: (dense index, value)
+  auto visit = [&](auto&& fn) {
+    if (staged) {
+      for (int d = tid; d < total; d += kSelThreads) fn(d, s_val[d]);
+    } else {
+      for (int sg = w; sg < nsegs; sg += kSelWaves) {
+        const int c0 = s_off[sg], c = s_off[sg + 1] - c0;
+        for (int j = lane; j < c; j += kWave) fn(c0 + j, sv[(int64_t)sg * kSegCols + j]);
+      }
+    }
+  };
+
+  // ---- radix select of the N-th largest key (k_topk's passes, on the passing scores only)
+  const bool take_all = total <= N;
+  if (!take_all) {
+    for (int pass = 0;; ++pass) {
+      int shift = 32 - kTkBits * (pass + 1), width = kTkBits;
+      if (shift < 0) { width += shift; shift = 0; }
+      const unsigned dmask = (1u << width) - 1u;
+      const unsigned prefix = s_prefix, mask = s_mask;
+      for (int b = tid; b < kTkBins; b += kSelThreads) s_hist[b] = 0;
+      __syncthreads();
+      visit([&](int, float v) {
+        const unsigned k = tk_key(v);
+        if ((k & mask) == prefix) atomicAdd(&s_hist[(k >> shift) & dmask], 1u);
+      });
+      __syncthreads();
+      const int g = kSelThreads - 1 - tid;
+      const int hi_c = (int)s_hist[2 * g + 1], lo_c = (int)s_hist[2 * g];
+      int in_prefix;
+      const int above = block_excl_sum(hi_c + lo_c, s_isum, &in_prefix);
+      const int need = s_need;
+      if (above < need && need <= above + hi_c + lo_c) {
+        const bool top = need <= above + hi_c;
+        const int b = top ? 2 * g + 1 : 2 * g;
+        const int bc = top ? hi_c : lo_c;
+        const int rem = need - (top ? above : above + hi_c);
+        s_prefix = prefix | ((unsigned)b << shift);
+        s_mask = mask | (dmask << shift);
+        s_need = rem;
+        s_eqcnt = bc;
+        s_done = (bc == rem || shift == 0) ? 1 : 0;
+      }
+      __syncthreads();
+      if (s_done) break;
+    }
+  }
+  const unsigned prefix = s_prefix, mask = s_mask;
+  const int need_eq = s_need;
+  const int nsel = take_all ? total : N;
+  int nsort = take_all ? total : (N - need_eq) + s_eqcnt;
+  int m2 = 1;
+  while (m2 < nsort) m2 <<= 1;
+  if (m2 <= M) {
+    // everything at or above the threshold fits the sort buffer: collect unordered, the sort by
+    // (-score, dense index) puts equal scores in scan order
+    visit([&](int d, float v) {
+      if (take_all || (tk_key(v) & mask) >= prefix) {
+        const int pos = atomicAdd(&s_cnt, 1);
+        s_key[pos] = -(double)v;
+        s_sec[pos] = d;
+        s_pay[pos] = d;
+      }
+    });
+  } else {
+    // many exactly equal scores at the threshold: ordered compaction over contiguous dense runs,
+    // equal scores taken in scan order
+    nsort = N;
+    const int per = (total + kSelThreads - 1) / kSelThreads;
+    const int d_lo = min(total, tid * per), d_hi = min(total, d_lo + per);
+    const int sg_lo = d_lo < d_hi ? tkc_seg(s_off, nsegs, d_lo) : 0;
+    auto walk = [&](auto&& fn) {
+      int sg = sg_lo;
+      for (int d = d_lo; d < d_hi; ++d) {
+        float v;
+        if (staged) {
+          v = s_val[d];
+        } else {
+          while (s_off[sg + 1] <= d) ++sg;
+          v = sv[(int64_t)sg * kSegCols + (d - s_off[sg])];
+        }
+        fn(d, v);
+      }
+    };
+    int n_above = 0, n_eq = 0;
+    // counters updated arithmetically: an if / else-if on two locals compiled to a store through
+    // a selected stack pointer (scratch)
+    walk([&](int, float v) {
+      const unsigned k = tk_key(v) & mask;
+      n_above += k > prefix ? 1 : 0;
+      n_eq += k == prefix ? 1 : 0;
+    });
+    int tot_above, tot_eq;
+    int pa = block_excl_sum(n_above, s_isum, &tot_above);
+    int pe = block_excl_sum(n_eq, s_isum, &tot_eq);
+    walk([&](int d, float v) {
+      const unsigned k = tk_key(v) & mask;
+      const bool ab = k > prefix, eq = k == prefix;
+      const int pos = ab ? pa : (eq && pe < need_eq ? tot_above + pe : -1);
+      pa += ab ? 1 : 0;
+      pe += eq ? 1 : 0;
+      if (pos >= 0) {
+        s_key[pos] = -(double)v;
+        s_sec[pos] = d;
+        s_pay[pos] = d;
+      }
+    });
+  }
+  __syncthreads();
+  bitonic(s_key, s_sec, s_pay, nsort);
+  if (tid == 0) {
+    a.cand_count[slot] = nsel;
+    a.warn[slot] = 0;
+  }
+  // dense index -> grid position (row, column) through the segment's column-order mask
+  for (int i = tid; i < nsel; i += kSelThreads) {
+    const int d = s_pay[i];
+    const int sg = tkc_seg(s_off, nsegs, d);
+    const int j = d - s_off[sg];
+    const uint64_t e = mk[2 * sg], o = mk[2 * sg + 1];
+    const uint64_t c0 = spread32((uint32_t)e) | (spread32((uint32_t)o) << 1);
+    const int n0 = __popcll(c0);
+    const int col = j < n0 ? select_bit(c0, j)
+                           : 64 + select_bit(spread32((uint32_t)(e >> 32)) | (spread32((uint32_t)(o >> 32)) << 1), j - n0);
+    const int row = sg / a.nseg;
+    a.cand[((int64_t)slot * a.N + i) * 2 + 0] = a.t0 + row;
+    a.cand[((int64_t)slot * a.N + i) * 2 + 1] = (sg - row * a.nseg) * kSegCols + col;
+    a.cand_score[(int64_t)slot * a.N + i] = -s_key[i];
+  }
+}
+
 }  // namespace
 
-// the compact layout needs k_score2 (whole-segment writes) and the reference selection (k_topk
-// reads the full grid)
-bool score_compact(const SyncLaunch& L) { return L.compact && !L.topk && score2_path(L); }
+// the compact layout needs k_score2 (whole-segment writes); top-k selection reads it through
+// k_topkc when the slot's segment offsets fit its LDS (else k_topk on the full grid)
+bool score_compact(const SyncLaunch& L) {
+  return L.compact && score2_path(L) && (!L.topk || (int64_t)L.NT * n_segments(L.NF) <= kTkcMaxSeg);
+}
 
 hipError_t launch_score(const SyncLaunch& L, hipStream_t s) {
   if (L.NT <= 0 || L.NF <= 0 || L.n_slots <= 0) return hipSuccess;
@@ -1058,6 +1291,25 @@ hipError_t launch_select(const SyncLaunch& L, hipStream_t s) {
   a.smask = L.smask;
   a.nseg = n_segments(a.NF);
   a.compact = score_compact(L) ? 1 : 0;
+  if (L.topk && a.compact) {
+    // LDS: histogram, segment offsets, the sort buffers (M >= N, a power of two) and as many staged
+    // scores as an 80 KB workgroup holds (two per CU), at least 4096
+    int M = 64;
+    while (M < L.N) M <<= 1;
+    const int nsegs = a.NT * a.nseg;
+    const size_t fixed = kTkBins * sizeof(unsigned) + (size_t)((nsegs + 2) & ~1) * sizeof(int) +
+                         (size_t)M * (sizeof(double) + 2 * sizeof(int));
+    const size_t budget = 80 * 1024;
+    const int V = (int)std::max<size_t>(4096, fixed < budget ? (budget - fixed) / sizeof(float) : 0);
+    const size_t lds = fixed + (size_t)V * sizeof(float);
+    if (lds > 64 * 1024) {
+      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k_topkc),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(k_topkc, dim3(L.n_slots), dim3(kSelThreads), lds, s, a, M, V);
+    return hipGetLastError();
+  }
   if (L.topk) {
     if (L.wf_f64)
       hipLaunchKernelGGL(k_topk<double>, dim3(L.n_slots), dim3(kSelThreads), 0, s, a);

@@ -158,6 +158,36 @@ def test_topk_selection_vs_oracle(golden, gpu, oracle):
     assert n >= 40
 
 
+def test_topk_compact_paths_vs_oracle(gpu, oracle):
+    """k_topkc (top-k from the compact score segments) on full-size 12 kHz waterfalls against
+    oracle.select_topk and against k_topk on the full grid (want_grid): passing scores staged in LDS
+    (min_score 2, ~10^4 passing) and streamed from HBM past the LDS budget (min_score -1000, every
+    grid point passes); quantised levels put thousands of exactly equal scores at the threshold,
+    which takes the ordered (scan-order) compaction instead of the unordered collection."""
+    from ft8_demodulator_amd import _device
+    rng = np.random.default_rng(77)
+    F, T = 1920, 186
+    cases = 0
+    for trial in range(4):
+        if trial < 2:   # ~20 k (streamed) and ~6.4 k (staged) scores >= 2
+            mag = (rng.standard_normal((F, T)) * (6.0 if trial == 0 else 4.0) - 60.0).astype(np.float32)
+        else:
+            mag = (rng.integers(0, 3, size=(F, T)) * 4.0 - 60.0).astype(np.float32)
+        grid = oracle.score_grid(mag, 2, 2)
+        NF = grid.shape[1]
+        for N, ms in ((300, 2), (300, -1000), (4096, 0.5), (1, -1000), (2000, 1)):
+            cands, _, warn = _device.sync_select(_wf(mag, 2, 2), N, ms, flags=1)
+            full, _, _ = _device.sync_select(_wf(mag, 2, 2), N, ms, want_grid=True, flags=1)
+            idx, sc = oracle.select_topk(grid, N, ms)
+            exp = [(int(i // NF) - 20, int(i % NF)) for i in idx]
+            assert [(a, b) for a, b, _ in cands] == exp, (trial, N, ms)
+            assert np.array_equal(np.array([s_ for _, _, s_ in cands], dtype=np.float64), sc), (trial, N, ms)
+            assert [(a, b) for a, b, _ in full] == exp, (trial, N, ms)
+            assert warn == 0
+            cases += 1
+    assert cases == 20
+
+
 def test_topk_ties_in_scan_order(gpu, oracle):
     """Silence scores exactly 0 everywhere: the top-k set is the first N grid points."""
     from ft8_demodulator_amd import _device
