@@ -328,8 +328,9 @@ def subtract_redecode(dev, n_slots=334, signals=50, iters=50, reps=3, oracle_sam
     if n_or:
         mism1, mism2, n1, n2 = [], [], 0, 0
         for s_ in range(n_or):
-            g1 = sorted(bytes(r["payload"]).hex() for r in recs[s_] if r["pass_index"] == 0)
-            g2 = sorted(bytes(r["payload"]).hex() for r in recs[s_] if r["pass_index"] == 1)
+            # payload SETS: a message decoded at two candidates appears twice in the records
+            g1 = sorted({bytes(r["payload"]).hex() for r in recs[s_] if r["pass_index"] == 0})
+            g2 = sorted({bytes(r["payload"]).hex() for r in recs[s_] if r["pass_index"] == 1})
             o1, o2 = oracle_sample[1][s_]
             n1, n2 = n1 + len(o1), n2 + len(o2)
             if g1 != o1:

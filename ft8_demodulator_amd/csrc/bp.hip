@@ -326,7 +326,8 @@ struct BpArgs {
   double* llr_out;
   uint8_t* plain_out;
   ft8_result* res;
-  unsigned* work;             // [claim counter, retired waves], both 0 between launches
+  unsigned long long* work;   // claim counter (64-bit, never reset)
+  unsigned long long work_base;  // this launch's first ticket (BpLaunch.work_base)
   unsigned long long* stats;  // nullable: [candidates, iterations entered, message passes, converged]
   int slot0;
   int tie_blocks;             // k_llr's first tie_blocks workgroups run tie_order
@@ -702,22 +703,17 @@ __global__ __launch_bounds__(kWave, kBpLbWaves) void k_bp(BpArgs a) {
   // candidate would serialise in L2)
   unsigned st_cand = 0, st_iter = 0, st_pass = 0, st_conv = 0;
   for (;;) {
-    unsigned item = 0;
-    if (lane == 0) item = atomicAdd(a.work, 1u);
+    unsigned long long ticket = 0;
+    if (lane == 0) ticket = atomicAdd(a.work, 1ull);
     // wave-uniform: candidate metadata then lives in SGPRs (scalar loads), not VGPRs
-    item = __builtin_amdgcn_readfirstlane(__shfl(item, 0));
-    if ((int)item >= a.n_items) {
-      // every wave's claims end with exactly one ticket >= n_items, after which it retires: the wave
-      // whose retirement comes last (work[1] reaches gridDim - 1) runs after every other claim and
-      // leaves both counters at 0 for the next launch -- no memset kernel per launch (a fresh
-      // counter buffer is zeroed once, capi.hip), and whatever value the claim counter ended at,
-      // e.g. after a launch that was cut short, the next completed launch resets it
-      if (lane == 0 && atomicAdd(a.work + 1, 1u) == gridDim.x - 1u) {
-        atomicExch(a.work, 0u);
-        atomicExch(a.work + 1, 0u);
-      }
-      break;
-    }
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)ticket);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(ticket >> 32));
+    // tickets of this launch start at work_base (host-advanced, see BpLaunch); a wave retires at
+    // its first ticket past the items -- no counter reset and no retire counter: round 3's
+    // last-retiring-wave reset put 4096 same-address atomics on the launch's tail
+    const unsigned long long rel = (((unsigned long long)hi << 32) | lo) - a.work_base;
+    if (rel >= (unsigned long long)a.n_items) break;
+    const unsigned item = (unsigned)rel;
 
     int slot = 0, at = 0, af = 0, cidx = 0;
     double score = 0.0;
@@ -991,6 +987,7 @@ constexpr int kPackThreads = 1024;
 __global__ __launch_bounds__(kPackThreads) void k_pack(const ft8_result* rec, const int32_t* counts, int n_slots,
                                                        int cap, int capacity, int slot_offset, uint8_t* send,
                                                        ft8_result* overflow) {
+  FT8_RACE_PROLOGUE();
   __shared__ int s_off[kPackThreads];
   __shared__ int s_wave[kPackThreads / kWave + 1];
   const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid >> 6;
@@ -1105,6 +1102,7 @@ BpArgs make_args(const BpLaunch& L) {
   a.plain_out = L.plain_out;
   a.res = L.res;
   a.work = L.work;
+  a.work_base = L.work_base ? *L.work_base : 0ull;
   a.stats = L.stats;
   a.slot0 = L.slot0;
   a.tie = TieArgs{L.n_slots, L.N, L.cand_count, L.warn, L.tie, L.cand_score};
@@ -1128,12 +1126,14 @@ hipError_t launch_llr(const BpLaunch& L, hipStream_t s) {
 hipError_t launch_bp(const BpLaunch& L, hipStream_t s) {
   if (L.n_items <= 0) return hipSuccess;
   BpArgs a = make_args(L);
-  // L.work is 0 here: zeroed when its buffer was allocated, and every k_bp launch leaves it at 0
   const int per_simd = max(1, min(L.grid_waves, kBpWavesPerSimd));
   const int waves = min(L.n_items, kBpGridCus * 4 * per_simd);  // resident waves, persistent
   if (L.mode == 0) hipLaunchKernelGGL(k_bp<false>, dim3(waves), dim3(kWave), 0, s, a);
   else hipLaunchKernelGGL(k_bp<true>, dim3(waves), dim3(kWave), 0, s, a);
-  return hipGetLastError();
+  const hipError_t e = hipGetLastError();
+  // the launch consumes n_items + waves tickets (every item once, then one per wave)
+  if (e == hipSuccess && L.work_base) *L.work_base += (unsigned long long)L.n_items + (unsigned long long)waves;
+  return e;
 }
 
 hipError_t launch_tie_apply(const TieArgs& a, int32_t* cand, double* cand_score, hipStream_t s) {

@@ -58,6 +58,9 @@ struct ft8_ctx {
   std::vector<PlanEntry> plans;
   std::vector<WinEntry> wins;
   DevBuf wf, scores, smask, cand, cand_score, cand_count, warn, rowsum, res_all, work, stats, llr, tie;
+  // first ticket of the next k_bp launch per claim counter in `work` (8 B each: [0] ft8_bp's, [1 + k]
+  // decode chunk k's); reset with the buffer, which is zeroed whenever it is (re)allocated
+  std::vector<unsigned long long> work_base;
   // FT8_FLAG_SUBTRACT: residual samples, per-record fits, pass-1 / pass-2 records
   DevBuf residual, sub_est, out1, counts1, out2, counts2;
   int sub_slots = 0, sub_cap = 0;  // shape of the fits in sub_est (ft8_subtract_fits)
@@ -124,6 +127,15 @@ int ensure_zeroed(ft8_ctx* c, DevBuf& b, size_t bytes, hipStream_t s) {
   if (rc || (b.p == old && b.cap == old_cap)) return rc;
   hipError_t e = hipMemsetAsync(b.p, 0, b.cap, s);
   return e == hipSuccess ? FT8_OK : hipfail(c, e, "memset");
+}
+
+// the k_bp claim counters (8 B each) and their host-side ticket bases
+int ensure_work(ft8_ctx* c, int n_counters, hipStream_t s) {
+  void* old = c->work.p;
+  int rc = ensure_zeroed(c, c->work, sizeof(unsigned long long) * (size_t)n_counters, s);
+  if (rc) return rc;
+  if (c->work.p != old) c->work_base.assign(c->work.cap / sizeof(unsigned long long), 0ull);
+  return FT8_OK;
 }
 
 int ensure(ft8_ctx* c, DevBuf& b, size_t bytes) {
@@ -626,8 +638,8 @@ int decode_pass(ft8_ctx* c, const void* d_samples, int dtype, int64_t n_samples,
   const int csz = (c->n_streams > 0 && c->chunk_slots > 0) ? c->chunk_slots : n_slots;
   const int n_chunks = (n_slots + csz - 1) / csz;
   const int n_str = (c->n_streams > 0 && n_chunks > 1) ? std::min(c->n_streams, n_chunks) : 0;
-  // k_bp counter pairs: [0, 1] belong to ft8_bp (a caller stream), [2 + 2k, 3 + 2k] to chunk k
-  if ((rc = ensure_zeroed(c, c->work, sizeof(unsigned) * 2 * (size_t)(n_chunks + 1), s))) return rc;
+  // k_bp claim counters: [0] belongs to ft8_bp (a caller stream), [1 + k] to chunk k
+  if ((rc = ensure_work(c, n_chunks + 1, s))) return rc;
   hipError_t e = hipSuccess;
   if (n_str > 0) {
     while ((int)c->streams.size() < n_str) {
@@ -683,7 +695,8 @@ int decode_pass(ft8_ctx* c, const void* d_samples, int dtype, int64_t n_samples,
     B.llr_out = (double*)c->llr.p + (size_t)FT8_LDPC_N * c0 * N;
     B.llr_in = B.llr_out;
     B.res = (ft8_result*)c->res_all.p + (size_t)c0 * N;
-    B.work = (unsigned*)c->work.p + 2 + 2 * k;
+    B.work = (unsigned long long*)c->work.p + 1 + k;
+    B.work_base = &c->work_base[1 + k];
     B.stats = (unsigned long long*)c->stats.p;
     B.grid_waves = n_str > 0 ? c->bp_waves : 8;  // clamped to the kernel's 4 resident waves per SIMD
     B.tie = tie;
@@ -1099,7 +1112,7 @@ int ft8_bp(ft8_ctx* c, const double* d_llr, int32_t n, int32_t max_iterations, u
   if (n <= 0) return FT8_OK;
   DeviceGuard dg(c->device);
   int rc;
-  if ((rc = ensure_zeroed(c, c->work, 16, (hipStream_t)stream))) return rc;  // counters [0, 1]: ft8_bp's own
+  if ((rc = ensure_work(c, 1, (hipStream_t)stream))) return rc;  // counter [0]: ft8_bp's own
   BpLaunch L{};
   L.mode = 2;
   L.llr_in = d_llr;
@@ -1108,7 +1121,8 @@ int ft8_bp(ft8_ctx* c, const double* d_llr, int32_t n, int32_t max_iterations, u
   L.max_iterations = max_iterations;
   L.plain_out = d_plain;
   L.res = d_res;
-  L.work = (unsigned*)c->work.p;
+  L.work = (unsigned long long*)c->work.p;
+  L.work_base = &c->work_base[0];
   L.stats = (unsigned long long*)c->stats.p;
   StageTimer tm(c, 3, (hipStream_t)stream);
   hipError_t e = launch_bp(L, (hipStream_t)stream);

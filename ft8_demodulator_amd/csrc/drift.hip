@@ -51,6 +51,7 @@ __device__ double block_sum(double v, double* red) {
 
 // ---- stage 1 ---------------------------------------------------------------------------------
 __global__ __launch_bounds__(kFitThreads) void k_drift_fit1(DriftFitLaunch a) {
+  FT8_RACE_PROLOGUE();
   __shared__ int s_idx[kDriftMaxT];
   __shared__ unsigned long long s_flag[kDriftMaxT / kWave];
   __shared__ double s_red[kFitWaves];
@@ -190,6 +191,7 @@ __global__ __launch_bounds__(kFitThreads) void k_drift_fit1(DriftFitLaunch a) {
 __device__ __forceinline__ int py_norm(int v, int T) { return v < 0 ? max(v + T, 0) : min(v, T); }
 
 __global__ __launch_bounds__(kFitThreads) void k_drift_fit2(DriftFitLaunch a) {
+  FT8_RACE_PROLOGUE();
   __shared__ int s_idx[kDriftMaxT];
   __shared__ double s_tmpl[kMaxTmpl];
   __shared__ double s_px[kMaxPts], s_py[kMaxPts];

@@ -10,6 +10,34 @@
 namespace ft8 {
 
 constexpr int kWave = 64;
+
+// ---- barrier-race check build (-DFT8_RACE_CHECK; tools/build_race.sh, never the shipped library) --
+// FT8_RACE_PROLOGUE() opens every kernel whose workgroup has more than one wave and uses LDS: the
+// whole LDS allocation of the workgroup (static + dynamic: the dispatch packet's
+// group_segment_size) is filled with 0xffffffff (a NaN / -1 sentinel), a barrier, then one wave of
+// the workgroup (rotating with the workgroup id) sleeps ~64 k cycles before it starts.  A read of
+// another wave's LDS staging that no barrier orders after the write then sees the sentinel instead
+// of a late value, deterministically, and the GPU tests fail.
+#ifdef FT8_RACE_CHECK
+__device__ __forceinline__ void race_prologue() {
+  const char* dp = (const char*)__builtin_amdgcn_dispatch_ptr();
+  const uint32_t bytes = *(const uint32_t*)(dp + 20);  // hsa_kernel_dispatch_packet_t.group_segment_size
+  const uint32_t nt = blockDim.x * blockDim.y * blockDim.z;
+  const uint32_t t = threadIdx.x + blockDim.x * (threadIdx.y + blockDim.y * threadIdx.z);
+  for (uint32_t off = 4 * t; off + 4 <= bytes; off += 4 * nt)
+    asm volatile("ds_write_b32 %0, %1" ::"v"(off), "v"(0xffffffffu) : "memory");
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+  const uint32_t nw = (nt + kWave - 1) / kWave;
+  if (nw > 1 && t / kWave == blockIdx.x % nw)
+    for (int i = 0; i < 8; ++i) __builtin_amdgcn_s_sleep(127);
+}
+#define FT8_RACE_PROLOGUE() ::ft8::race_prologue()
+#else
+#define FT8_RACE_PROLOGUE() \
+  do {                      \
+  } while (0)
+#endif
 constexpr int kMaxCandidates = 4096;   // LDS-resident selection (k_select)
 // LDS FFT limits (one (P + P/16 + 1)-point buffer per frame, 256 threads holding P / 256 values each
 // per stage): float32 P <= 10240 (87 KB), float64 P <= 8192 (139 KB).  Larger or non-2/3/5/7 lengths
@@ -160,7 +188,12 @@ struct BpLaunch {
   double* llr_out;         // k_llr output [n_items][174]
   uint8_t* plain_out;      // nullable [n_items][174]
   ft8_result* res;         // nullable [n_items]
-  unsigned* work;          // k_bp: 2 counters [claim, retired], 0 between launches (k_bp resets them)
+  // k_bp claim counter: 64-bit, never reset.  Launch j claims tickets [base_j, base_j + n_items +
+  // waves): every item once, then one ticket >= n_items per wave, so the host advances the base
+  // (*work_base, host memory, one per counter) by n_items + waves at each launch -- no reset, no
+  // retire counter, nothing a launch cut short could leave behind for the next one to skip over
+  unsigned long long* work;
+  unsigned long long* work_base;
   unsigned long long* stats = nullptr;  // [candidates, iterations entered, message passes, converged]
   int slot0 = 0;           // batch index of slot 0 (records carry slot0 + local slot)
   int grid_waves = 4;      // k_bp persistent grid: resident waves per SIMD (clamped to 4)

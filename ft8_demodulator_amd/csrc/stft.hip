@@ -341,6 +341,7 @@ template <typename InT, bool CPLX, typename CT, int MAXV>
 // CU; the radix-16/15 stages then fit 256 VGPRs), one for the 8192- and 10240-point variants (a
 // 16384-point float32 variant, 64 values per thread, trips a gfx950 code-generation error)
 __global__ __launch_bounds__(kThreads, (MAXV <= 16 ? 2 : 1)) void k_stft(StftArgs a) {
+  FT8_RACE_PROLOGUE();
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   cplx<CT>* buf = reinterpret_cast<cplx<CT>*>(smem);
   // XCD-aware order: hardware deals workgroup ids round-robin over the 8 XCDs, so consecutive
@@ -477,6 +478,7 @@ __device__ __forceinline__ cplx<CT> load_c(const InT* x, int64_t n) {
 // for the dB one's fifteen inlined float64 log10)
 template <typename InT, typename CT, int M, bool AMAX>
 __global__ __launch_bounds__(kC38Threads, 2) void k_stftc3840(StftArgs a) {
+  FT8_RACE_PROLOGUE();
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   cplx<CT>* buf = reinterpret_cast<cplx<CT>*>(smem);
   CT* sv = reinterpret_cast<CT*>(smem + (size_t)(kC38P + kC38P / 16 + 1) * sizeof(cplx<CT>));
@@ -653,6 +655,7 @@ constexpr int kDftReseed = 32;
 
 template <typename InT, bool CPLX, typename CT>
 __global__ __launch_bounds__(kDftThreads) void k_stft_dft(StftArgs a) {
+  FT8_RACE_PROLOGUE();
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   cplx<CT>* z = reinterpret_cast<cplx<CT>*>(smem);
   const int nbb = (a.nf_out + kDftThreads - 1) / kDftThreads;
@@ -741,6 +744,7 @@ struct BlueArgs {
 
 template <typename InT, bool CPLX, typename CT, int MAXV>
 __global__ __launch_bounds__(kThreads, 1) void k_stft_blue(BlueArgs b) {
+  FT8_RACE_PROLOGUE();
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   cplx<CT>* buf = reinterpret_cast<cplx<CT>*>(smem);
   const StftArgs& a = b.s;

@@ -228,6 +228,7 @@ __device__ __forceinline__ void lds_st(f2* p, f2 v) { *(volatile lds_f2*)p = v; 
 
 template <typename InT>
 __global__ __launch_bounds__(kThreads38) void k_stft3840p(Args a) {
+  FT8_RACE_PROLOGUE();
   __shared__ f2 buf[2][kBuf];  // frame A, frame B
   __shared__ f2 wl[kP / 2];    // the window as pairs (w[2n], w[2n+1]): 39.4 KB in all, four workgroups per CU
   const int t = threadIdx.x;

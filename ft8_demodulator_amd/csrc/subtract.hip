@@ -58,6 +58,7 @@ __device__ __forceinline__ float ramp_f(int n, int L, int nsps) { return tx::gfs
 
 template <typename InT>
 __global__ __launch_bounds__(kSubThreads) void k_sub_est(SubLaunch a) {
+  FT8_RACE_PROLOGUE();
   // dynamic LDS: the decimated baseband z (phases 2-3), then the float pulse table (phase 4)
   extern __shared__ float4 s_dyn[];
   float2* s_z = reinterpret_cast<float2*>(s_dyn);
@@ -333,6 +334,7 @@ constexpr int kApTile = kSubThreads * kApPer;
 
 template <typename InT>
 __global__ __launch_bounds__(kSubThreads) void k_sub_apply(SubLaunch a) {
+  FT8_RACE_PROLOGUE();
   __shared__ int s_E[tx::kExt];
   __shared__ float2 s_A[tx::kSymbols];
   __shared__ float s_ph0[tx::kSymbols + 1];

@@ -68,6 +68,7 @@ __device__ __forceinline__ bool passes(T s, double ms, int cmp_f64) {
 
 template <typename T, bool LDS, int TW>
 __global__ __launch_bounds__(kScoreThreads) void k_score(ScoreArgs a) {
+  FT8_RACE_PROLOGUE();
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   T* tile = reinterpret_cast<T*>(smem);
   const int slot = blockIdx.y;
@@ -246,6 +247,7 @@ __device__ __forceinline__ void s2_load(const float* wf, int T, int F, int a0, i
 // time+1).
 template <int BPT, int SPS, bool COMPACT>
 __global__ __launch_bounds__(kS2Threads) void k_score2(ScoreArgs a) {
+  FT8_RACE_PROLOGUE();
   static_assert(kS2TW == kSegCols, "a workgroup's columns are one score segment");
   using G = S2Geom<BPT, SPS>;
   constexpr int P = G::P;
@@ -573,6 +575,7 @@ __device__ __forceinline__ int seg_rank(uint64_t e, uint64_t o, int col) {
 
 template <typename T>
 __global__ __launch_bounds__(kSelThreads) void k_select(SelectArgs a) {
+  FT8_RACE_PROLOGUE();
   __shared__ double s_key[kMaxCandidates + 2];
   __shared__ int s_sec[kMaxCandidates + 2];
   __shared__ int s_pay[kMaxCandidates + 2];
@@ -883,6 +886,7 @@ template <> struct TkKey<double> {
 
 template <typename T>
 __global__ __launch_bounds__(kSelThreads) void k_topk(SelectArgs a) {
+  FT8_RACE_PROLOGUE();
   using K = typename TkKey<T>::K;
   __shared__ double s_key[kMaxCandidates + 2];
   __shared__ int s_sec[kMaxCandidates + 2];
@@ -1043,6 +1047,7 @@ __device__ __forceinline__ int tkc_seg(const int* off, int nsegs, int d) {
 }
 
 __global__ __launch_bounds__(kSelThreads) void k_topkc(SelectArgs a, int M, int V) {
+  FT8_RACE_PROLOGUE();
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int nsegs = a.NT * a.nseg;
   unsigned* s_hist = reinterpret_cast<unsigned*>(smem);

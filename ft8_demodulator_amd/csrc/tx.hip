@@ -37,6 +37,7 @@ __device__ int lower_slot(const ft8_tx_signal* sig, int n, int s) {
 
 template <bool CPLX, typename OT, typename AT>
 __global__ __launch_bounds__(kSynThreads) void k_synth(SynthLaunch a) {
+  FT8_RACE_PROLOGUE();
   __shared__ int s_E[tx::kExt];
   __shared__ int s_PS[tx::kExt + 1];
   __shared__ int s_range[2];

@@ -48,8 +48,9 @@ def main():
         f, w = fetch.get(k), write.get(k)
         out[k] = {"fetch_bytes_raw": f, "fetch_bytes_x2": 2 * f if f is not None else None, "write_bytes": w,
                   "hbm_bytes": (2 * f if f is not None else 0) + (w or 0)}
-    json.dump({"build_id": build_id(), "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE passes of tools/bp_only.py "
-                         "(256 slots, config 3); FETCH_SIZE doubled per the gfx950 correction",
+    what = sys.argv[4] if len(sys.argv) > 4 else "tools/bp_only.py (256 slots, config 3)"
+    json.dump({"build_id": build_id(), "source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE passes of {what}; "
+                         "FETCH_SIZE doubled per the gfx950 correction; bytes per launch (mean over dispatches)",
                "kernels": out}, open(sys.argv[3], "w"), indent=1)
     for k, v in out.items():
         print(k, {a: (round(b / 1e6, 2) if b else b) for a, b in v.items()}, "MB")
