@@ -28,6 +28,7 @@ namespace ft8 {
 namespace {
 
 constexpr int kSubThreads = 256;
+constexpr int kSubRecStride = 32;               // k_sub_est workgroups per slot
 constexpr int kSubWaves = kSubThreads / kWave;
 constexpr int kMaxQ = 32;
 constexpr int kMaxHyp = 1024;
@@ -72,14 +73,17 @@ __global__ __launch_bounds__(kSubThreads) void k_sub_est(SubLaunch a) {
   __shared__ float2 s_A[tx::kSymbols];
   __shared__ int s_flag;
 
-  // records of one slot on one XCD (workgroup id % 8)
+  // records of one slot on one XCD (workgroup id % 8); kSubRecStride workgroups per slot, each
+  // taking records rec0, rec0 + kSubRecStride, ... (a slot decodes ~20: one record per workgroup,
+  // instead of round 3's one workgroup per record slot of the capacity, ~93 % of them empty)
   const int w = blockIdx.x;
   const int j8 = w / 8;
-  const int slot = (w % 8) + 8 * (j8 / a.cap);
-  const int rec = j8 % a.cap;
+  const int slot = (w % 8) + 8 * (j8 / kSubRecStride);
+  const int rec0 = j8 % kSubRecStride;
   if (slot >= a.n_slots) return;
   const int cnt = min(a.counts[slot], a.cap);
-  if (rec >= cnt) return;
+  for (int rec = rec0; rec < cnt; rec += kSubRecStride) {
+  __syncthreads();  // the previous record's LDS reads are done
   SubEst* est = reinterpret_cast<SubEst*>(a.est) + (int64_t)slot * a.cap + rec;
   const ft8_result* rs = a.res + (int64_t)slot * a.cap;
   const ft8_result r = rs[rec];
@@ -94,7 +98,7 @@ __global__ __launch_bounds__(kSubThreads) void k_sub_est(SubLaunch a) {
   dup = __syncthreads_or(dup);
   if (!r.ok || dup) {
     if (threadIdx.x == 0) est->active = 0;
-    return;
+    continue;
   }
   if (threadIdx.x < kWave) tx::encode_tones_wave(r.payload, threadIdx.x, s_tones);
   __syncthreads();
@@ -327,66 +331,116 @@ __global__ __launch_bounds__(kSubThreads) void k_sub_est(SubLaunch a) {
     est->f0 = f0;
     est->active = 1;
   }
+  }  // records
 }
 
 constexpr int kApPer = 16;
 constexpr int kApTile = kSubThreads * kApPer;
+constexpr int kApFits = 8;                     // fits staged in LDS per batch
+constexpr int kApList = 1024;                  // overlapping fits listed per pass over the records
 
+// One workgroup per (slot, tile of 4096 samples).  Wave 0 lists the fits that overlap the tile, in
+// record order; their parameters (tones as floats, amplitudes, symbol phases, start, f0) are staged
+// kApFits at a time; every thread then adds each staged fit's waveform to its 16 samples.  A
+// thread's samples are 256 apart, so its symbol index k and in-symbol offset i advance by one
+// addition each (one floor division per fit and thread instead of one per sample).
 template <typename InT>
 __global__ __launch_bounds__(kSubThreads) void k_sub_apply(SubLaunch a) {
   FT8_RACE_PROLOGUE();
-  __shared__ int s_E[tx::kExt];
-  __shared__ float2 s_A[tx::kSymbols];
-  __shared__ float s_ph0[tx::kSymbols + 1];
+  __shared__ float s_E[kApFits][tx::kExt];
+  __shared__ float2 s_A[kApFits][tx::kSymbols];
+  __shared__ float s_ph0[kApFits][tx::kSymbols + 1];
+  __shared__ long long s_start[kApFits];
+  __shared__ float s_f0r[kApFits];
+  __shared__ short s_list[kApList];
+  __shared__ int s_nlist;
   extern __shared__ float s_Pf[];  // float pulse table [3 nsps + 1]
-  bool staged = false;
   const int slot = blockIdx.y;
   const int64_t t0 = (int64_t)blockIdx.x * kApTile;
   const int nsps = a.nsps, L = tx::kSymbols * nsps;
-  const float fsf = (float)a.fs;
+  const float fsf = (float)a.fs, inv_nsps = 1.0f / (float)nsps, sr = 6.25f / fsf;
   const int cnt = min(a.counts[slot], a.cap);
   const SubEst* est = reinterpret_cast<const SubEst*>(a.est) + (int64_t)slot * a.cap;
   float acc[kApPer];
 #pragma unroll
   for (int k = 0; k < kApPer; ++k) acc[k] = 0.f;
-  for (int j = 0; j < cnt; ++j) {
-    const SubEst* e = est + j;
-    if (!e->active) continue;
-    const int64_t start = e->start;
-    if (start >= t0 + kApTile || start + L <= t0) continue;
-    __syncthreads();
-    if (!staged) {
-      for (int i = threadIdx.x; i <= 3 * nsps; i += kSubThreads) s_Pf[i] = a.Pf[i];
-      staged = true;
-    }
-    if (threadIdx.x < tx::kExt) {
-      const int jj = (int)threadIdx.x - 1;
-      s_E[threadIdx.x] = e->tones[jj < 0 ? 0 : (jj > tx::kSymbols - 1 ? tx::kSymbols - 1 : jj)];
-    }
-    if (threadIdx.x < tx::kSymbols) s_A[threadIdx.x] = make_float2(e->amp[threadIdx.x][0], e->amp[threadIdx.x][1]);
-    if (threadIdx.x <= tx::kSymbols) s_ph0[threadIdx.x] = e->phase0[threadIdx.x];
-    __syncthreads();
-    const float f0r = (float)(e->f0 / (double)a.fs), sr = 6.25f / fsf;
-#pragma unroll
-    for (int kk = 0; kk < kApPer; ++kk) {
-      const int64_t nabs = t0 + threadIdx.x + (int64_t)kk * kSubThreads;
-      const int64_t nr64 = nabs - start;
-      if (nr64 < 0 || nr64 >= L || nabs >= a.n_samples) continue;
-      const int nr = (int)nr64;
-      const int k = nr / nsps, i = nr - k * nsps;
-      const float cyc = s_ph0[k] + (float)i * f0r + sr * dG(s_E, s_Pf, nsps, k, i);
-      const float fr = __builtin_amdgcn_fractf(cyc);  // v_sin / v_cos take revolutions
-      const float sn = __builtin_amdgcn_sinf(fr), cs = __builtin_amdgcn_cosf(fr);
-      const float t = ((float)i + 0.5f) / (float)nsps - 0.5f;  // position from the symbol centre
-      float2 A;
-      if (t < 0.f) {
-        const float2 p = s_A[k > 0 ? k - 1 : 0], c = s_A[k];
-        A = make_float2(c.x + t * (c.x - p.x), c.y + t * (c.y - p.y));
-      } else {
-        const float2 c = s_A[k], nx = s_A[k < tx::kSymbols - 1 ? k + 1 : k];
-        A = make_float2(c.x + t * (nx.x - c.x), c.y + t * (nx.y - c.y));
+  for (int i = threadIdx.x; i <= 3 * nsps; i += kSubThreads) s_Pf[i] = a.Pf[i];
+  for (int j0 = 0; j0 < cnt; j0 += kApList) {
+    __syncthreads();  // the previous list is consumed
+    if (threadIdx.x < kWave) {
+      // the fits of records [j0, j0 + kApList) that overlap this tile, in record order
+      const int lane = threadIdx.x;
+      int n = 0;
+      for (int jb = j0; jb < min(cnt, j0 + kApList); jb += kWave) {
+        const int j = jb + lane;
+        bool hit = false;
+        if (j < cnt && est[j].active) {
+          const int64_t st = est[j].start;
+          hit = st < t0 + kApTile && st + L > t0;
+        }
+        const uint64_t m = __ballot(hit);
+        if (hit) s_list[n + __popcll(m & ((1ull << lane) - 1ull))] = (short)(j - j0);
+        n += __popcll(m);
       }
-      acc[kk] += ramp_f(nr, L, nsps) * (A.x * cs - A.y * sn);
+      if (lane == 0) s_nlist = n;
+    }
+    __syncthreads();
+    const int nl = s_nlist;
+    for (int b0 = 0; b0 < nl; b0 += kApFits) {
+      const int nb = min(kApFits, nl - b0);
+      __syncthreads();  // the previous batch is consumed
+      for (int q = threadIdx.x; q < nb * tx::kExt; q += kSubThreads) {
+        const int f = q / tx::kExt, kk = q - f * tx::kExt;
+        const SubEst* e = est + j0 + s_list[b0 + f];
+        const int jj = kk - 1;
+        s_E[f][kk] = (float)e->tones[jj < 0 ? 0 : (jj > tx::kSymbols - 1 ? tx::kSymbols - 1 : jj)];
+      }
+      for (int q = threadIdx.x; q < nb * tx::kSymbols; q += kSubThreads) {
+        const int f = q / tx::kSymbols, kk = q - f * tx::kSymbols;
+        const SubEst* e = est + j0 + s_list[b0 + f];
+        s_A[f][kk] = make_float2(e->amp[kk][0], e->amp[kk][1]);
+      }
+      for (int q = threadIdx.x; q < nb * (tx::kSymbols + 1); q += kSubThreads) {
+        const int f = q / (tx::kSymbols + 1), kk = q - f * (tx::kSymbols + 1);
+        s_ph0[f][kk] = est[j0 + s_list[b0 + f]].phase0[kk];
+      }
+      if (threadIdx.x < nb) {
+        const SubEst* e = est + j0 + s_list[b0 + threadIdx.x];
+        s_start[threadIdx.x] = e->start;
+        s_f0r[threadIdx.x] = (float)(e->f0 / (double)a.fs);
+      }
+      __syncthreads();
+      for (int f = 0; f < nb; ++f) {
+        const int64_t start = s_start[f];
+        const float f0r = s_f0r[f];
+        const float* E = s_E[f];
+        const int nr0 = (int)(t0 + threadIdx.x - start);  // |nr0| < 2^31: slots hold < 2^31 samples
+        int k = nr0 >= 0 ? nr0 / nsps : -((-nr0 + nsps - 1) / nsps);  // floor
+        int i = nr0 - k * nsps;
+#pragma unroll
+        for (int kk = 0; kk < kApPer; ++kk) {
+          const int64_t nabs = t0 + threadIdx.x + (int64_t)kk * kSubThreads;
+          if (k >= 0 && k < tx::kSymbols && nabs < a.n_samples) {
+            // dG of tx_device.h's pulse table (the same float operations as dG())
+            const float g = E[k] * (s_Pf[i + 2 * nsps] - s_Pf[2 * nsps]) + E[k + 1] * (s_Pf[i + nsps] - s_Pf[nsps]) +
+                            E[k + 2] * (s_Pf[i] - s_Pf[0]);
+            const float cyc = s_ph0[f][k] + (float)i * f0r + sr * g;
+            const float fr = __builtin_amdgcn_fractf(cyc);  // v_sin / v_cos take revolutions
+            const float sn = __builtin_amdgcn_sinf(fr), cs = __builtin_amdgcn_cosf(fr);
+            const float t = ((float)i + 0.5f) * inv_nsps - 0.5f;  // position from the symbol centre
+            const float2 c = s_A[f][k];
+            const float2 o = t < 0.f ? s_A[f][k > 0 ? k - 1 : 0] : s_A[f][k < tx::kSymbols - 1 ? k + 1 : k];
+            const float2 A = t < 0.f ? make_float2(c.x + t * (c.x - o.x), c.y + t * (c.y - o.y))
+                                     : make_float2(c.x + t * (o.x - c.x), c.y + t * (o.y - c.y));
+            acc[kk] += ramp_f(k * nsps + i, L, nsps) * (A.x * cs - A.y * sn);
+          }
+          i += kSubThreads;
+          while (i >= nsps) {
+            i -= nsps;
+            ++k;
+          }
+        }
+      }
     }
   }
   const InT* x = reinterpret_cast<const InT*>(a.x) + (int64_t)slot * a.slot_stride;
@@ -443,7 +497,7 @@ hipError_t launch_subtract(const SubLaunch& a, hipStream_t s) {
   if (a.n_slots <= 0 || a.n_samples <= 0) return hipSuccess;
   if (a.Q <= 0 || a.Q > kMaxQ || a.nsps % a.Q != 0 || a.hop <= 0 || a.nsps % a.hop != 0) return hipErrorInvalidValue;
   if (a.cap > 0) {
-    const unsigned grid = (unsigned)(((a.n_slots + 7) / 8) * 8 * (int64_t)a.cap);
+    const unsigned grid = (unsigned)(((a.n_slots + 7) / 8) * 8 * (int64_t)kSubRecStride);
     const size_t mz = (size_t)tx::kSymbols * a.Q + 2 * (a.Q / (2 * (a.nsps / a.hop)) + 2);
     const size_t lds = std::max(mz * sizeof(float2), (size_t)(3 * a.nsps + 1) * sizeof(float));
     if (a.dtype == FT8_I16)
