@@ -284,7 +284,9 @@ def subtract_oracle_worker(args):
     res = OS.residual(xs, ofit, plan.nperseg, 12000).astype(np.float32)
     p1 = {pay for pay, _, _ in d1}
     new = {pay for pay, _, _ in OS.decode_topk(res, 12000, 300, 2, iters)} - p1
-    return xs, sorted(p.hex() for p in p1), sorted(p.hex() for p in new), sum(f is not None for f in ofit)
+    from oracle import oracle as O
+    n_pass = int((O.score_grid(O.waterfall(xs, 12000, 2, 2), 2, 2) >= 2).sum())  # k_topkc's input size
+    return xs, sorted(p.hex() for p in p1), sorted(p.hex() for p in new), sum(f is not None for f in ofit), n_pass
 
 
 def subtract_oracle(n, procs, signals=50, iters=50):
@@ -297,7 +299,8 @@ def subtract_oracle(n, procs, signals=50, iters=50):
     with ctx.Pool(min(procs, n), initializer=_worker_init) as pool:
         out = pool.map(subtract_oracle_worker, [(SUB_SEED0 + b, signals, iters) for b in range(n)], chunksize=1)
     return (np.stack([o[0] for o in out]), [(o[1], o[2]) for o in out],
-            {"fits": sum(o[3] for o in out), "oracle_wall_s": time.perf_counter() - t0})
+            {"fits": sum(o[3] for o in out), "oracle_wall_s": time.perf_counter() - t0,
+             "passing_scores_per_slot": float(np.mean([o[4] for o in out]))})
 
 
 def subtract_redecode(dev, n_slots=334, signals=50, iters=50, reps=3, oracle_sample=None):
@@ -357,7 +360,45 @@ def subtract_redecode(dev, n_slots=334, signals=50, iters=50, reps=3, oracle_sam
     ctx.set_timing(False)
     tm = ctx.timing(reset=True)
     cn = ctx.counters(reset=True)
+    n_samp = int(x.shape[1])
     del x
+    # rooflines of the second-pass kernels (algorithmic work per unit).  Fits:
+    # one per distinct pass-1 payload of a slot (k_sub_est skips failed records and repeats)
+    fits = sum(len({bytes(r["payload"]) for r in recs[s_] if r["pass_index"] == 0}) for s_ in range(n_slots))
+    nsps, Q, hop = 1920, 32, 960
+    D = nsps // Q
+    Mt = -(-(hop // 2) // D)
+    nT, nF, Mz = 2 * Mt + 1, 5, 79 * Q + 2 * (Mt + 1)
+    est_flops = Mz * D * 10 + nF * 79 * (Q * 14 + (nT - 1) * 19 + nT * 3) + 79 * nsps * 16
+    app_flops = 79 * nsps * 28
+    FP32_PEAK = 157.3
+
+    def ms_of(k_):
+        v = tm.get(k_, (0.0, 0))
+        return v[0] / max(v[1], 1)
+    est_ms, app_ms, sel_ms = ms_of("sub_est"), ms_of("sub_apply"), ms_of("select")
+    rl = {}
+    if est_ms > 0:
+        a_ = fits * est_flops / (est_ms * 1e-3) / 1e12
+        rl["k_sub_est"] = {"bound": "fp32-valu", "achieved": a_, "peak": FP32_PEAK, "unit": "TFLOP/s",
+                           "frac": a_ / FP32_PEAK, "flops_per_fit": est_flops, "fits_per_launch": fits,
+                           "launch_ms": est_ms}
+    if app_ms > 0:
+        a_ = fits * app_flops / (app_ms * 1e-3) / 1e12
+        hbm_b = n_slots * n_samp * 8  # samples read + residual written once
+        rl["k_sub_apply"] = {"bound": "fp32-valu", "achieved": a_, "peak": FP32_PEAK, "unit": "TFLOP/s",
+                             "frac": a_ / FP32_PEAK, "flops_per_fit": app_flops, "fits_per_launch": fits,
+                             "launch_ms": app_ms, "hbm_bytes_per_launch": hbm_b,
+                             "hbm_frac": hbm_b / (app_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+    if sel_ms > 0 and oracle_sample is not None:
+        nseg = 88 * 15
+        npass = oracle_sample[2]["passing_scores_per_slot"]
+        b_ = n_slots * (nseg * 16 + npass * 4 + 300 * 16)
+        rl["k_topkc"] = {"bound": "hbm", "achieved": b_ / (sel_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": b_ / (sel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "bytes_per_launch": b_,
+                         "launch_ms": sel_ms,
+                         "bytes": "per slot: 1320 segment masks x 16 B + passing scores x 4 B (mean of the oracle "
+                                  "sample's slots) + 300 candidates x 16 B written"}
     return {"workload": f"BASELINE config 4 with subtract-and-redecode: {n_slots} crowded slots x K=300 "
                         f"(top-k selection) = {n_slots * 300} candidates per pass, {iters} BP iterations, "
                         "pass 1 -> fit and subtract every decoded message -> pass 2 on the residual",
@@ -366,6 +407,7 @@ def subtract_redecode(dev, n_slots=334, signals=50, iters=50, reps=3, oracle_sam
             "true_decodes_per_slot_pass1": true1 / n_slots, "true_decodes_per_slot_pass2": true2 / n_slots,
             "false_decodes": int(false),
             "parity": parity,
+            "rooflines": rl,
             "stages_ms": {k: v[0] / reps for k, v in tm.items() if v[1] > 0},
             "data": "synthetic (ft8_demodulator_amd.synth, seeds 200000..); the reference has no second pass: "
                     "pass 2 is pinned against the CPU restatement oracle/subtract.py "

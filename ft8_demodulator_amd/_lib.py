@@ -19,9 +19,9 @@ FT8_OK, FT8_E_ARG, FT8_E_HIP, FT8_E_UNSUPPORTED, FT8_E_NOMEM, FT8_E_RANGE = 0, -
 FT8_FLAG_TOPK, FT8_FLAG_SUBTRACT = 1, 2
 FT8_TX_PROTOCOL, FT8_TX_REFERENCE = 0, 1
 FT8_STFT_STOCKHAM, FT8_STFT_PACKED3840, FT8_STFT_CHIRPZ, FT8_STFT_DFT = 0, 1, 2, 3
-N_STAGES = 11
-STAGE_NAMES = ("stft", "score", "select", "bp", "compact", "decode_batch", "llr", "subtract",
-               "drift_stft_argmax", "drift_fit", "drift_derotate")
+N_STAGES = 12
+STAGE_NAMES = ("stft", "score", "select", "bp", "compact", "decode_batch", "llr", "sub_est",
+               "drift_stft_argmax", "drift_fit", "drift_derotate", "sub_apply")
 # ft8_drift_status
 (FT8_DRIFT_PENDING, FT8_DRIFT_NO_SEGMENT, FT8_DRIFT_LINEAR, FT8_DRIFT_FEW_POINTS, FT8_DRIFT_DEGREE,
  FT8_DRIFT_FULL, FT8_DRIFT_UNDERDETERMINED) = range(7)

@@ -804,8 +804,12 @@ int subtract_core(ft8_ctx* c, const void* x, int dtype, float* resid, int64_t n_
   L.est = c->sub_est.p;
   L.Q = Q;
   StageTimer tm(c, 7, s);
-  hipError_t e = launch_subtract(L, s);
+  hipError_t e = launch_sub_est(L, s);
   tm.done();
+  if (e != hipSuccess) return hipfail(c, e, "subtract launch");
+  StageTimer tm2(c, 11, s);
+  e = launch_sub_apply(L, s);
+  tm2.done();
   if (e != hipSuccess) return hipfail(c, e, "subtract launch");
   c->sub_slots = n_slots;
   c->sub_cap = cap;

@@ -255,7 +255,8 @@ struct SubLaunch {
   int Q;                       // decimated samples per symbol (nsps % Q == 0)
 };
 size_t sub_est_bytes();        // sizeof one SubEst record
-hipError_t launch_subtract(const SubLaunch& a, hipStream_t s);
+hipError_t launch_sub_est(const SubLaunch& a, hipStream_t s);    // fits of the records (k_sub_est)
+hipError_t launch_sub_apply(const SubLaunch& a, hipStream_t s);  // residual = x - fitted signals
 
 // out[slot] = the pass-1 records out1[slot][0 .. counts1) followed by the pass-2 records
 // out2[slot][0 .. counts2) whose payload no pass-1 record carries (pass_index = 1); counts uncapped

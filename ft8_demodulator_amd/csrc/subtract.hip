@@ -493,7 +493,7 @@ __global__ __launch_bounds__(kWave) void k_merge(ft8_result* out, int32_t* count
 
 size_t sub_est_bytes() { return sizeof(SubEst); }
 
-hipError_t launch_subtract(const SubLaunch& a, hipStream_t s) {
+hipError_t launch_sub_est(const SubLaunch& a, hipStream_t s) {
   if (a.n_slots <= 0 || a.n_samples <= 0) return hipSuccess;
   if (a.Q <= 0 || a.Q > kMaxQ || a.nsps % a.Q != 0 || a.hop <= 0 || a.nsps % a.hop != 0) return hipErrorInvalidValue;
   if (a.cap > 0) {
@@ -504,9 +504,13 @@ hipError_t launch_subtract(const SubLaunch& a, hipStream_t s) {
       hipLaunchKernelGGL(k_sub_est<int16_t>, dim3(grid), dim3(kSubThreads), lds, s, a);
     else
       hipLaunchKernelGGL(k_sub_est<float>, dim3(grid), dim3(kSubThreads), lds, s, a);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
+    return hipGetLastError();
   }
+  return hipSuccess;
+}
+
+hipError_t launch_sub_apply(const SubLaunch& a, hipStream_t s) {
+  if (a.n_slots <= 0 || a.n_samples <= 0) return hipSuccess;
   dim3 g2((unsigned)((a.n_samples + kApTile - 1) / kApTile), (unsigned)a.n_slots);
   const size_t lds2 = (size_t)(3 * a.nsps + 1) * sizeof(float);
   if (a.dtype == FT8_I16)

@@ -364,8 +364,9 @@ const char* ft8_build_flags(void);
 int ft8_replay_stage(ft8_ctx* ctx, int32_t stage, int32_t reps, void* stream);
 
 /* ---- per-stage device timing (HIP events on the caller's stream) --------------------------- */
-#define FT8_N_STAGES 11 /* 0 stft, 1 score, 2 select, 3 bp, 4 compact, 5 whole decode_batch, 6 llr,
-                         7 subtract, 8 drift STFT-argmax, 9 drift fits, 10 drift de-rotation */
+#define FT8_N_STAGES 12 /* 0 stft, 1 score, 2 select, 3 bp, 4 compact, 5 whole decode_batch, 6 llr,
+                         7 subtraction fits (k_sub_est), 8 drift STFT-argmax, 9 drift fits,
+                         10 drift de-rotation, 11 subtraction of the fitted signals (k_sub_apply) */
 int ft8_set_timing(ft8_ctx* ctx, int enable);
 /* which stages record events while timing is enabled (bit s = stage s; default all): timing one
  * stage at a time brackets only that kernel, so the rest of the step runs undisturbed */
