@@ -23,6 +23,9 @@ Prints ONE JSON line on rank 0.  Besides the contract fields it carries:
   bp_stress     BASELINE config 4 first pass: 100k LLR vectors x 50 BP iterations, candidates/s (N=1)
   subtract_redecode  BASELINE config 4 with the subtract-and-redecode second pass: 334 crowded
                 slots x K=300 (top-k), 50 iterations, both passes, candidates/s (N=1)
+  geometries    the reference's other geometries (20 kHz, the bundled recording's rate; 12 kHz at
+                bins_per_tone = steps_per_symbol = 10, its decode test's): slots/s, stage times, the
+                generic STFT / score kernels' HBM rooflines (N=1)
   drift_correct the beacon receiver's frequency-drift correction on a batch of 256
                 complex128 beacon signals (12 kHz, 3 x 12.64 s, steps_per_symbol 8): signals/s, the
                 dominant kernel's roofline and the oracle port's CPU rate (N=1)
@@ -414,6 +417,73 @@ def subtract_redecode(dev, n_slots=334, signals=50, iters=50, reps=3, oracle_sam
                     "(tests/test_gpu_subtract_oracle.py)"}
 
 
+# the reference's own geometries besides the 12 kHz production one: the bundled recording's 20 kHz
+# (from_wave.py:24-69, src/ft8_tools/ft8_beacon_receiver/data/raw/ft8_fs20k_f0_550_id_1.wav) and its
+# decode test's 12 kHz at bins_per_tone = steps_per_symbol = 10 (test_spectrogram_analyse.py:128-163)
+GEOMETRIES = (("fs20k_bpt2", 20000, 2, 2, 256), ("fs12k_bpt10", 12000, 10, 10, 32))
+
+
+def geometry_legs(dev, reps=5):
+    """Decode throughput at the reference's other geometries (K=300, min_score=2, 20 iterations),
+    with the per-stage event times and the HBM rooflines of the generic STFT and score kernels they
+    run.  Parity at these geometries is the test suite's (tests/test_gpu_reftests.py: the
+    reference's own outputs)."""
+    import torch
+    from ft8_demodulator_amd import SlotDecoder, synth, _lib
+    out = {}
+    for name, fs, bpt, sps, n in GEOMETRIES:
+        x, _ = synth.make_slots(n, 50, fs=fs, snr_db=(-24.0, -10.0), seed=300000, device=dev)
+        dec = SlotDecoder(fs, bpt, sps, 300, 2, 20, device=dev)
+        ctx = dec.ctx
+        ctx.set_timing(True)
+        ctx.set_timing(False)
+        for _ in range(3):
+            _, counts = dec.run(x)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            _, counts = dec.run(x)
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / reps
+        decodes = int(counts.sum())
+        stages = {}
+        for st in ("stft", "score", "select", "llr", "bp"):
+            ctx.timing(reset=True)
+            ctx.set_timing(True, stages=[st])
+            for _ in range(3):
+                dec.run(x)
+            torch.cuda.synchronize()
+            ctx.set_timing(False)
+            v = ctx.timing(reset=True)[st]
+            stages[st] = v[0] / max(v[1], 1)
+        ctx.set_timing(False, stages=None)
+        N = int(x.shape[1])
+        pl = dec.plan(N)
+        method = _lib.lib().ft8_stft_method(ctx.handle, fs, bpt, sps, N, _lib.FT8_F32)
+        wf_bytes = n * pl.T * pl.F * 4
+        stft_b = n * N * 4 + wf_bytes
+        out[name] = {
+            "workload": f"{n} synthetic 15-s slots at {fs} Hz, bins_per_tone {bpt}, steps_per_symbol {sps} "
+                        f"(nfft {pl.nfft}, hop {pl.hop}: {pl.T} frames x {pl.F} bins), 50 signals/slot, "
+                        "K=300, min_score=2, 20 iterations",
+            "slots_per_s": n / dt, "ms_per_batch": dt * 1e3, "decodes_per_batch": decodes,
+            "stft_method": {0: "stockham", 1: "packed3840", 2: "chirp-z", 3: "direct DFT"}.get(method, method),
+            "score_kernel": "k_score2" if bpt == sps and bpt <= 4 else "k_score",
+            "stages_ms": stages,
+            "roofline_stft": {"bound": "hbm", "bytes_per_launch": stft_b, "launch_ms": stages["stft"],
+                              "achieved": stft_b / (stages["stft"] * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                              "unit": "GB/s", "frac": stft_b / (stages["stft"] * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                              "bytes": "samples read once (4 B) + dB waterfall written once (4 B per kept bin)"},
+            "roofline_score": {"bound": "hbm", "bytes_per_launch": wf_bytes, "launch_ms": stages["score"],
+                               "achieved": wf_bytes / (stages["score"] * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                               "unit": "GB/s", "frac": wf_bytes / (stages["score"] * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                               "bytes": "the waterfall read once (score writes not counted)"},
+            "data": "synthetic (ft8_demodulator_amd.synth, seeds 300000..)"}
+        del x, dec
+        torch.cuda.empty_cache()
+    return out
+
+
 DRIFT_PARAMS = {"bins_per_tone": 2, "steps_per_symbol": 8}  # the reference test's correction params
 
 
@@ -752,6 +822,7 @@ def main():
     ap.add_argument("--subtract-oracle-slots", type=int, default=8,
                     help="slots of the subtract leg checked against oracle/subtract.py (0: none)")
     ap.add_argument("--no-drift", action="store_true", help="skip the frequency-drift correction leg")
+    ap.add_argument("--no-geometries", action="store_true", help="skip the 20 kHz / bpt=10 geometry legs")
     ap.add_argument("--gather", action="store_true",
                     help="N = 1: every timed step also packs its decodes and all-gathers them over a world-size-1 "
                          "RCCL group (the per-step exchange of the N > 1 path)")
@@ -977,6 +1048,9 @@ def main():
         drift = drift_correct(dev)
         drift["cpu_baseline"] = drift_cpu_port
         drift["rate_32768"] = drift_32k(dev)
+    geoms = None
+    if world == 1 and not args.no_geometries:
+        geoms = geometry_legs(dev)
     sub = None
     if world == 1 and not args.no_subtract:
         sub = subtract_redecode(dev, oracle_sample=sub_oracle)
@@ -1059,6 +1133,7 @@ def main():
         "single_call": call,
         "subtract_redecode": sub,
         "drift_correct": drift,
+        "geometries": geoms,
         "cpu_baseline": cpu,
         "parity": parity,
         "reference_measured": REFERENCE_MEASURED,

@@ -57,7 +57,11 @@ __device__ __forceinline__ float dG(const int* E, const float* Pf, int nsps, int
 
 __device__ __forceinline__ float ramp_f(int n, int L, int nsps) { return tx::gfsk_ramp<float>(n, L, nsps, 0); }
 
-template <typename InT>
+// REST = false: workgroup rec0 of a slot fits record rec0 (no loop: 168 VGPRs, three waves per
+// SIMD); REST = true: the records past kSubRecStride, rec0 + kSubRecStride, rec0 + 2 kSubRecStride,
+// ... (a loop over records lets the compiler keep loop-invariant values live: 256 VGPRs), a second
+// launch whose workgroups exit at once unless a slot decoded more than kSubRecStride messages
+template <typename InT, bool REST>
 __global__ __launch_bounds__(kSubThreads) void k_sub_est(SubLaunch a) {
   FT8_RACE_PROLOGUE();
   // dynamic LDS: the decimated baseband z (phases 2-3), then the float pulse table (phase 4)
@@ -82,7 +86,7 @@ __global__ __launch_bounds__(kSubThreads) void k_sub_est(SubLaunch a) {
   const int rec0 = j8 % kSubRecStride;
   if (slot >= a.n_slots) return;
   const int cnt = min(a.counts[slot], a.cap);
-  for (int rec = rec0; rec < cnt; rec += kSubRecStride) {
+  for (int rec = rec0 + (REST ? kSubRecStride : 0); rec < cnt; rec += kSubRecStride) {
   __syncthreads();  // the previous record's LDS reads are done
   SubEst* est = reinterpret_cast<SubEst*>(a.est) + (int64_t)slot * a.cap + rec;
   const ft8_result* rs = a.res + (int64_t)slot * a.cap;
@@ -98,6 +102,7 @@ __global__ __launch_bounds__(kSubThreads) void k_sub_est(SubLaunch a) {
   dup = __syncthreads_or(dup);
   if (!r.ok || dup) {
     if (threadIdx.x == 0) est->active = 0;
+    if (!REST) break;
     continue;
   }
   if (threadIdx.x < kWave) tx::encode_tones_wave(r.payload, threadIdx.x, s_tones);
@@ -126,51 +131,56 @@ __global__ __launch_bounds__(kSubThreads) void k_sub_est(SubLaunch a) {
   const double fmix = ftone + 3.5 * 6.25;
 
   // ---- 2. mixed-down, box-car decimated baseband z[m], samples [nb + m D, nb + (m + 1) D).  A
-  // thread owns z[tid + 256 j], j < kZ, and walks their D samples together, kB at a time, so
-  // kZ * kB independent loads are in flight per round trip
+  // thread owns z[tid + 256 j], j < kZ, in two halves of kZh, and walks a half's D samples
+  // together, kB at a time, so kZh * kB independent loads are in flight per round trip (the whole
+  // kZ at once held ~70 more VGPRs: two waves per SIMD instead of three)
   {
     constexpr int kZ = (tx::kSymbols * kMaxQ + 2 * (kMaxQ / 2 + 2) + kSubThreads - 1) / kSubThreads;
+    constexpr int kZh = (kZ + 1) / 2;
     constexpr int kB = 2;
     const int64_t nb = s0 - (int64_t)Mg * D;
     float ss, sc;
     sincospif((float)(-2.0 * fmix / fs), &ss, &sc);
     const float2 step = make_float2(sc, ss);
-    float2 wv[kZ], acc[kZ];
+#pragma unroll 1
+    for (int h = 0; h < 2; ++h) {
+      float2 wv[kZh], acc[kZh];
 #pragma unroll
-    for (int j = 0; j < kZ; ++j) {
-      const int64_t n0 = nb + (int64_t)(threadIdx.x + j * kSubThreads) * D;
-      const double cyc = fmix * (double)n0 / fs;
-      float ws, wc;
-      sincospif((float)(-2.0 * (cyc - floor(cyc))), &ws, &wc);
-      wv[j] = make_float2(wc, ws);
-      acc[j] = make_float2(0.f, 0.f);
-    }
-    for (int i0 = 0; i0 < D; i0 += kB) {
-      float v[kZ][kB];
+      for (int jj = 0; jj < kZh; ++jj) {
+        const int64_t n0 = nb + (int64_t)(threadIdx.x + (h * kZh + jj) * kSubThreads) * D;
+        const double cyc = fmix * (double)n0 / fs;
+        float ws, wc;
+        sincospif((float)(-2.0 * (cyc - floor(cyc))), &ws, &wc);
+        wv[jj] = make_float2(wc, ws);
+        acc[jj] = make_float2(0.f, 0.f);
+      }
+      for (int i0 = 0; i0 < D; i0 += kB) {
+        float v[kZh][kB];
 #pragma unroll
-      for (int j = 0; j < kZ; ++j) {
-        const int m = threadIdx.x + j * kSubThreads;
-        const int64_t n0 = nb + (int64_t)m * D + i0;
+        for (int jj = 0; jj < kZh; ++jj) {
+          const int m = threadIdx.x + (h * kZh + jj) * kSubThreads;
+          const int64_t n0 = nb + (int64_t)m * D + i0;
 #pragma unroll
-        for (int u = 0; u < kB; ++u) {
-          const int64_t n = n0 + u;
-          v[j][u] = (m < Mz && i0 + u < D && n >= 0 && n < a.n_samples) ? ld_sample<InT>(x, n) : 0.f;
+          for (int u = 0; u < kB; ++u) {
+            const int64_t n = n0 + u;
+            v[jj][u] = (m < Mz && i0 + u < D && n >= 0 && n < a.n_samples) ? ld_sample<InT>(x, n) : 0.f;
+          }
+        }
+#pragma unroll
+        for (int jj = 0; jj < kZh; ++jj) {
+#pragma unroll
+          for (int u = 0; u < kB; ++u) {
+            acc[jj].x += v[jj][u] * wv[jj].x;
+            acc[jj].y += v[jj][u] * wv[jj].y;
+            wv[jj] = make_float2(wv[jj].x * step.x - wv[jj].y * step.y, wv[jj].x * step.y + wv[jj].y * step.x);
+          }
         }
       }
 #pragma unroll
-      for (int j = 0; j < kZ; ++j) {
-#pragma unroll
-        for (int u = 0; u < kB; ++u) {
-          acc[j].x += v[j][u] * wv[j].x;
-          acc[j].y += v[j][u] * wv[j].y;
-          wv[j] = make_float2(wv[j].x * step.x - wv[j].y * step.y, wv[j].x * step.y + wv[j].y * step.x);
-        }
+      for (int jj = 0; jj < kZh; ++jj) {
+        const int m = threadIdx.x + (h * kZh + jj) * kSubThreads;
+        if (m < Mz) s_z[m] = acc[jj];
       }
-    }
-#pragma unroll
-    for (int j = 0; j < kZ; ++j) {
-      const int m = threadIdx.x + j * kSubThreads;
-      if (m < Mz) s_z[m] = acc[j];
     }
   }
   __syncthreads();
@@ -331,6 +341,7 @@ __global__ __launch_bounds__(kSubThreads) void k_sub_est(SubLaunch a) {
     est->f0 = f0;
     est->active = 1;
   }
+  if (!REST) break;
   }  // records
 }
 
@@ -500,10 +511,13 @@ hipError_t launch_sub_est(const SubLaunch& a, hipStream_t s) {
     const unsigned grid = (unsigned)(((a.n_slots + 7) / 8) * 8 * (int64_t)kSubRecStride);
     const size_t mz = (size_t)tx::kSymbols * a.Q + 2 * (a.Q / (2 * (a.nsps / a.hop)) + 2);
     const size_t lds = std::max(mz * sizeof(float2), (size_t)(3 * a.nsps + 1) * sizeof(float));
-    if (a.dtype == FT8_I16)
-      hipLaunchKernelGGL(k_sub_est<int16_t>, dim3(grid), dim3(kSubThreads), lds, s, a);
-    else
-      hipLaunchKernelGGL(k_sub_est<float>, dim3(grid), dim3(kSubThreads), lds, s, a);
+    if (a.dtype == FT8_I16) {
+      hipLaunchKernelGGL((k_sub_est<int16_t, false>), dim3(grid), dim3(kSubThreads), lds, s, a);
+      if (a.cap > kSubRecStride) hipLaunchKernelGGL((k_sub_est<int16_t, true>), dim3(grid), dim3(kSubThreads), lds, s, a);
+    } else {
+      hipLaunchKernelGGL((k_sub_est<float, false>), dim3(grid), dim3(kSubThreads), lds, s, a);
+      if (a.cap > kSubRecStride) hipLaunchKernelGGL((k_sub_est<float, true>), dim3(grid), dim3(kSubThreads), lds, s, a);
+    }
     return hipGetLastError();
   }
   return hipSuccess;
