@@ -392,7 +392,14 @@ __global__ __launch_bounds__(kThreads, (MAXV <= 16 ? 2 : 1)) void k_stft(StftArg
   };
   if (a.argmax == nullptr) {
     CT* out = reinterpret_cast<CT*>(a.out) + ((int64_t)slot * a.nt_out + fi) * a.nf_out;
-    for (int i = threadIdx.x; i < a.nf_out; i += kThreads) out[i] = db_of(level(i));
+    if constexpr (sizeof(CT) == 4) {
+      // 10 log10(v) = (10 log10 2) log2(v): v_log_f32 on a normal argument (v >= 1e-12), as
+      // k_stft3840p; log10f's correctly rounded libm sequence took ~25 VALU per bin
+      constexpr float kDb = 3.0102999566398119521f;
+      for (int i = threadIdx.x; i < a.nf_out; i += kThreads) out[i] = kDb * __builtin_amdgcn_logf(level(i));
+    } else {
+      for (int i = threadIdx.x; i < a.nf_out; i += kThreads) out[i] = db_of(level(i));
+    }
     return;
   }
   // argmax (np.argmax of the dB row) in one pass on the levels (level_better)

@@ -28,7 +28,7 @@ namespace ft8 {
 namespace {
 
 constexpr int kSubThreads = 256;
-constexpr int kSubRecStride = 32;               // k_sub_est workgroups per slot
+constexpr int kSubRecStride = 64;               // k_sub_est workgroups per slot (a crowded slot: ~40 records)
 constexpr int kSubWaves = kSubThreads / kWave;
 constexpr int kMaxQ = 32;
 constexpr int kMaxHyp = 1024;

@@ -1298,13 +1298,14 @@ hipError_t launch_select(const SyncLaunch& L, hipStream_t s) {
   a.compact = score_compact(L) ? 1 : 0;
   if (L.topk && a.compact) {
     // LDS: histogram, segment offsets, the sort buffers (M >= N, a power of two) and as many staged
-    // scores as an 80 KB workgroup holds (two per CU), at least 4096
+    // scores as fit beside them in 79 KB (two workgroups per CU: 160 KB less the static words; at
+    // 80 KB only one was resident), at least 4096
     int M = 64;
     while (M < L.N) M <<= 1;
     const int nsegs = a.NT * a.nseg;
     const size_t fixed = kTkBins * sizeof(unsigned) + (size_t)((nsegs + 2) & ~1) * sizeof(int) +
                          (size_t)M * (sizeof(double) + 2 * sizeof(int));
-    const size_t budget = 80 * 1024;
+    const size_t budget = 79 * 1024;
     const int V = (int)std::max<size_t>(4096, fixed < budget ? (budget - fixed) / sizeof(float) : 0);
     const size_t lds = fixed + (size_t)V * sizeof(float);
     if (lds > 64 * 1024) {
