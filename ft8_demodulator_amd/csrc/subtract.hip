@@ -131,56 +131,63 @@ __global__ __launch_bounds__(kSubThreads) void k_sub_est(SubLaunch a) {
   const double fmix = ftone + 3.5 * 6.25;
 
   // ---- 2. mixed-down, box-car decimated baseband z[m], samples [nb + m D, nb + (m + 1) D).  A
-  // thread owns z[tid + 256 j], j < kZ, in two halves of kZh, and walks a half's D samples
-  // together, kB at a time, so kZh * kB independent loads are in flight per round trip (the whole
-  // kZ at once held ~70 more VGPRs: two waves per SIMD instead of three)
+  // thread owns z[tid + 256 j], j < kZ, two at a time, and loads kDc samples of each before it
+  // accumulates them in sample order (2 kDc loads in flight per round trip: four round trips per
+  // pair at D = 60; round 3's two-sample steps over all of a thread's z took ~60 round trips; 32
+  // samples of each z in flight held 172 VGPRs, 16 hold 108: four waves per SIMD)
   {
     constexpr int kZ = (tx::kSymbols * kMaxQ + 2 * (kMaxQ / 2 + 2) + kSubThreads - 1) / kSubThreads;
-    constexpr int kZh = (kZ + 1) / 2;
-    constexpr int kB = 2;
+    constexpr int kDc = 16;
     const int64_t nb = s0 - (int64_t)Mg * D;
     float ss, sc;
     sincospif((float)(-2.0 * fmix / fs), &ss, &sc);
     const float2 step = make_float2(sc, ss);
 #pragma unroll 1
-    for (int h = 0; h < 2; ++h) {
-      float2 wv[kZh], acc[kZh];
+    for (int j0 = 0; j0 < kZ; j0 += 2) {
+      float2 wv[2], acc[2];
+      int m[2];
 #pragma unroll
-      for (int jj = 0; jj < kZh; ++jj) {
-        const int64_t n0 = nb + (int64_t)(threadIdx.x + (h * kZh + jj) * kSubThreads) * D;
+      for (int q = 0; q < 2; ++q) {
+        m[q] = threadIdx.x + (j0 + q) * kSubThreads;
+        const int64_t n0 = nb + (int64_t)m[q] * D;
         const double cyc = fmix * (double)n0 / fs;
         float ws, wc;
         sincospif((float)(-2.0 * (cyc - floor(cyc))), &ws, &wc);
-        wv[jj] = make_float2(wc, ws);
-        acc[jj] = make_float2(0.f, 0.f);
+        wv[q] = make_float2(wc, ws);
+        acc[q] = make_float2(0.f, 0.f);
       }
-      for (int i0 = 0; i0 < D; i0 += kB) {
-        float v[kZh][kB];
+      if (m[0] >= Mz) break;
+      for (int i0 = 0; i0 < D; i0 += kDc) {
+        float v[2][kDc];
 #pragma unroll
-        for (int jj = 0; jj < kZh; ++jj) {
-          const int m = threadIdx.x + (h * kZh + jj) * kSubThreads;
-          const int64_t n0 = nb + (int64_t)m * D + i0;
+        for (int q = 0; q < 2; ++q) {
+          // samples [n0 + lo, n0 + hi) of this chunk exist: one base pointer, immediate offsets
+          const int64_t n0 = nb + (int64_t)m[q] * D + i0;
+          const bool zok = m[q] < Mz && j0 + q < kZ;
+          const int lo = (int)min<int64_t>(kDc, max<int64_t>(0, -n0));
+          const int hi = zok ? (int)max<int64_t>(0, min<int64_t>(min(kDc, D - i0), a.n_samples - n0)) : 0;
+          const InT* xp = x + n0;
 #pragma unroll
-          for (int u = 0; u < kB; ++u) {
-            const int64_t n = n0 + u;
-            v[jj][u] = (m < Mz && i0 + u < D && n >= 0 && n < a.n_samples) ? ld_sample<InT>(x, n) : 0.f;
+          for (int u = 0; u < kDc; ++u) {
+            v[q][u] = 0.f;
+            if (u >= lo && u < hi) v[q][u] = ld_sample<InT>(xp, u);
           }
         }
 #pragma unroll
-        for (int jj = 0; jj < kZh; ++jj) {
+        for (int q = 0; q < 2; ++q) {
 #pragma unroll
-          for (int u = 0; u < kB; ++u) {
-            acc[jj].x += v[jj][u] * wv[jj].x;
-            acc[jj].y += v[jj][u] * wv[jj].y;
-            wv[jj] = make_float2(wv[jj].x * step.x - wv[jj].y * step.y, wv[jj].x * step.y + wv[jj].y * step.x);
+          for (int u = 0; u < kDc; ++u) {
+            if (i0 + u < D) {
+              acc[q].x += v[q][u] * wv[q].x;
+              acc[q].y += v[q][u] * wv[q].y;
+              wv[q] = make_float2(wv[q].x * step.x - wv[q].y * step.y, wv[q].x * step.y + wv[q].y * step.x);
+            }
           }
         }
       }
 #pragma unroll
-      for (int jj = 0; jj < kZh; ++jj) {
-        const int m = threadIdx.x + (h * kZh + jj) * kSubThreads;
-        if (m < Mz) s_z[m] = acc[jj];
-      }
+      for (int q = 0; q < 2; ++q)
+        if (m[q] < Mz && j0 + q < kZ) s_z[m[q]] = acc[q];
     }
   }
   __syncthreads();
@@ -278,9 +285,9 @@ __global__ __launch_bounds__(kSubThreads) void k_sub_est(SubLaunch a) {
   __syncthreads();
 
   // ---- 4. complex amplitude per symbol (one wave per symbol at a time; a lane's samples of the
-  // symbol are loaded kPf at a time before they are used)
+  // symbol are loaded kPf at a time before they are used: one round trip per symbol for nsps <= 2048)
   {
-    constexpr int kPf = 16;
+    constexpr int kPf = 32;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const float f0r = (float)(f0 / fs), sr = (float)(6.25 / fs);
     for (int k = wv; k < tx::kSymbols; k += kSubWaves) {
@@ -290,11 +297,13 @@ __global__ __launch_bounds__(kSubThreads) void k_sub_est(SubLaunch a) {
       const bool inside = nsym >= 0 && nsym + nsps <= a.n_samples;
       for (int i0 = lane; i0 < nsps; i0 += kPf * kWave) {
         float v[kPf];
+        const InT* xp = x + nsym + i0;
 #pragma unroll
         for (int u = 0; u < kPf; ++u) {
           const int i = i0 + u * kWave;
           const int64_t n = nsym + i;
-          v[u] = (i < nsps && (inside || (n >= 0 && n < a.n_samples))) ? ld_sample<InT>(x, n) : 0.f;
+          v[u] = 0.f;
+          if (i < nsps && (inside || (n >= 0 && n < a.n_samples))) v[u] = ld_sample<InT>(xp, u * kWave);
         }
 #pragma unroll
         for (int u = 0; u < kPf; ++u) {
