@@ -29,6 +29,7 @@ namespace {
 
 constexpr int kSubThreads = 256;
 constexpr int kSubRecStride = 64;               // k_sub_est workgroups per slot (a crowded slot: ~40 records)
+constexpr int kSubRestStride = 8;               // ... and per slot in the rest launch (records >= 64)
 constexpr int kSubWaves = kSubThreads / kWave;
 constexpr int kMaxQ = 32;
 constexpr int kMaxHyp = 1024;
@@ -57,9 +58,9 @@ __device__ __forceinline__ float dG(const int* E, const float* Pf, int nsps, int
 
 __device__ __forceinline__ float ramp_f(int n, int L, int nsps) { return tx::gfsk_ramp<float>(n, L, nsps, 0); }
 
-// REST = false: workgroup rec0 of a slot fits record rec0 (no loop: 168 VGPRs, three waves per
-// SIMD); REST = true: the records past kSubRecStride, rec0 + kSubRecStride, rec0 + 2 kSubRecStride,
-// ... (a loop over records lets the compiler keep loop-invariant values live: 256 VGPRs), a second
+// REST = false: workgroup rec0 of a slot fits record rec0 (no loop: 108 VGPRs, four waves per
+// SIMD); REST = true: the records past kSubRecStride, kSubRecStride + rec0 + j kSubRestStride (a
+// loop over records lets the compiler keep loop-invariant values live: ~170 VGPRs), a second
 // launch whose workgroups exit at once unless a slot decoded more than kSubRecStride messages
 template <typename InT, bool REST>
 __global__ __launch_bounds__(kSubThreads) void k_sub_est(SubLaunch a) {
@@ -82,11 +83,12 @@ __global__ __launch_bounds__(kSubThreads) void k_sub_est(SubLaunch a) {
   // instead of round 3's one workgroup per record slot of the capacity, ~93 % of them empty)
   const int w = blockIdx.x;
   const int j8 = w / 8;
-  const int slot = (w % 8) + 8 * (j8 / kSubRecStride);
-  const int rec0 = j8 % kSubRecStride;
+  constexpr int kStride = REST ? kSubRestStride : kSubRecStride;
+  const int slot = (w % 8) + 8 * (j8 / kStride);
+  const int rec0 = j8 % kStride;
   if (slot >= a.n_slots) return;
   const int cnt = min(a.counts[slot], a.cap);
-  for (int rec = rec0 + (REST ? kSubRecStride : 0); rec < cnt; rec += kSubRecStride) {
+  for (int rec = rec0 + (REST ? kSubRecStride : 0); rec < cnt; rec += kStride) {
   __syncthreads();  // the previous record's LDS reads are done
   SubEst* est = reinterpret_cast<SubEst*>(a.est) + (int64_t)slot * a.cap + rec;
   const ft8_result* rs = a.res + (int64_t)slot * a.cap;
@@ -518,14 +520,17 @@ hipError_t launch_sub_est(const SubLaunch& a, hipStream_t s) {
   if (a.Q <= 0 || a.Q > kMaxQ || a.nsps % a.Q != 0 || a.hop <= 0 || a.nsps % a.hop != 0) return hipErrorInvalidValue;
   if (a.cap > 0) {
     const unsigned grid = (unsigned)(((a.n_slots + 7) / 8) * 8 * (int64_t)kSubRecStride);
+    // the rest launch: 8 workgroups per slot, 2 700 near-empty ones at 334 slots (0.04 ms; at 64 per
+    // slot its 21 500 empty workgroups took 0.31 ms of wave launches)
+    const unsigned grid_rest = (unsigned)(((a.n_slots + 7) / 8) * 8 * (int64_t)kSubRestStride);
     const size_t mz = (size_t)tx::kSymbols * a.Q + 2 * (a.Q / (2 * (a.nsps / a.hop)) + 2);
     const size_t lds = std::max(mz * sizeof(float2), (size_t)(3 * a.nsps + 1) * sizeof(float));
     if (a.dtype == FT8_I16) {
       hipLaunchKernelGGL((k_sub_est<int16_t, false>), dim3(grid), dim3(kSubThreads), lds, s, a);
-      if (a.cap > kSubRecStride) hipLaunchKernelGGL((k_sub_est<int16_t, true>), dim3(grid), dim3(kSubThreads), lds, s, a);
+      if (a.cap > kSubRecStride) hipLaunchKernelGGL((k_sub_est<int16_t, true>), dim3(grid_rest), dim3(kSubThreads), lds, s, a);
     } else {
       hipLaunchKernelGGL((k_sub_est<float, false>), dim3(grid), dim3(kSubThreads), lds, s, a);
-      if (a.cap > kSubRecStride) hipLaunchKernelGGL((k_sub_est<float, true>), dim3(grid), dim3(kSubThreads), lds, s, a);
+      if (a.cap > kSubRecStride) hipLaunchKernelGGL((k_sub_est<float, true>), dim3(grid_rest), dim3(kSubThreads), lds, s, a);
     }
     return hipGetLastError();
   }
