@@ -62,7 +62,7 @@ struct ft8_ctx {
   // decode chunk k's); reset with the buffer, which is zeroed whenever it is (re)allocated
   std::vector<unsigned long long> work_base;
   // FT8_FLAG_SUBTRACT: residual samples, per-record fits, pass-1 / pass-2 records
-  DevBuf residual, sub_est, out1, counts1, out2, counts2;
+  DevBuf residual, sub_est, sub_list, out1, counts1, out2, counts2;
   int sub_slots = 0, sub_cap = 0;  // shape of the fits in sub_est (ft8_subtract_fits)
   // cumulative GFSK pulse of the transmit chain for one nsps (double and float)
   int gfsk_nsps = 0;
@@ -783,6 +783,7 @@ int subtract_core(ft8_ctx* c, const void* x, int dtype, float* resid, int64_t n_
     return fail(c, FT8_E_UNSUPPORTED, "subtraction needs nsps with a divisor in [8, 32] and hop | nsps");
   if ((rc = gfsk_tables(c, g.nperseg))) return rc;
   if ((rc = ensure(c, c->sub_est, sub_est_bytes() * (size_t)n_slots * (size_t)(cap > 0 ? cap : 1)))) return rc;
+  if ((rc = ensure(c, c->sub_list, sizeof(int32_t) * (size_t)n_slots * (size_t)(cap + 1)))) return rc;
   SubLaunch L{};
   L.x = x;
   L.dtype = dtype;
@@ -802,6 +803,7 @@ int subtract_core(ft8_ctx* c, const void* x, int dtype, float* resid, int64_t n_
   L.P = (const double*)c->gfsk_P.p;
   L.Pf = (const float*)c->gfsk_Pf.p;
   L.est = c->sub_est.p;
+  L.list = (int32_t*)c->sub_list.p;
   L.Q = Q;
   StageTimer tm(c, 7, s);
   hipError_t e = launch_sub_est(L, s);
@@ -980,7 +982,7 @@ int ft8_destroy(ft8_ctx* c) {
   {
     DeviceGuard dg(c->device);
     for (auto* b : {&c->wf, &c->scores, &c->smask, &c->cand, &c->cand_score, &c->cand_count, &c->warn, &c->rowsum,
-                    &c->res_all, &c->work, &c->stats, &c->llr, &c->tie, &c->residual, &c->sub_est, &c->out1,
+                    &c->res_all, &c->work, &c->stats, &c->llr, &c->tie, &c->residual, &c->sub_est, &c->sub_list, &c->out1,
                     &c->counts1, &c->out2, &c->counts2, &c->gfsk_P, &c->gfsk_Pf, &c->drift_idx, &c->drift_tmpl})
       if (b->p) (void)hipFree(b->p);
     for (auto& p : c->plans) {

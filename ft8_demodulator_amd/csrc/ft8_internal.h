@@ -253,6 +253,8 @@ struct SubLaunch {
   const float* Pf;             // the same in float
   void* est;                   // scratch [n_slots * cap] SubEst records
   int Q;                       // decimated samples per symbol (nsps % Q == 0)
+  int32_t* list;               // scratch [n_slots][cap + 1]: the records to fit (ok, first of their
+                               // payload in the slot), in record order, then their count
 };
 size_t sub_est_bytes();        // sizeof one SubEst record
 hipError_t launch_sub_est(const SubLaunch& a, hipStream_t s);    // fits of the records (k_sub_est)

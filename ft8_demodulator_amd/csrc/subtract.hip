@@ -28,8 +28,8 @@ namespace ft8 {
 namespace {
 
 constexpr int kSubThreads = 256;
-constexpr int kSubRecStride = 64;               // k_sub_est workgroups per slot (a crowded slot: ~40 records)
-constexpr int kSubRestStride = 8;               // ... and per slot in the rest launch (records >= 64)
+constexpr int kSubRecStride = 32;               // k_sub_est workgroups per slot (a crowded slot: ~21 fits)
+constexpr int kSubRestStride = 8;               // ... and per slot in the rest launch (fits >= 32)
 constexpr int kSubWaves = kSubThreads / kWave;
 constexpr int kMaxQ = 32;
 constexpr int kMaxHyp = 1024;
@@ -57,6 +57,38 @@ __device__ __forceinline__ float dG(const int* E, const float* Pf, int nsps, int
 }
 
 __device__ __forceinline__ float ramp_f(int n, int L, int nsps) { return tx::gfsk_ramp<float>(n, L, nsps, 0); }
+
+// k_sub_list: one wave per slot lists the records worth a fit -- ok, and the first record of the
+// slot carrying its payload (a crowded top-k slot decodes ~40 records for ~21 distinct messages) --
+// in record order, and marks every record inactive (k_sub_est then activates the ones it fits), so
+// k_sub_est's workgroups index fits directly instead of one workgroup per record testing itself
+__global__ __launch_bounds__(kWave) void k_sub_list(SubLaunch a) {
+  const int slot = blockIdx.x, lane = threadIdx.x;
+  const int cnt = min(a.counts[slot], a.cap);
+  const ft8_result* rs = a.res + (int64_t)slot * a.cap;
+  SubEst* est = reinterpret_cast<SubEst*>(a.est) + (int64_t)slot * a.cap;
+  int32_t* list = a.list + (int64_t)slot * (a.cap + 1);
+  int n = 0;
+  for (int j0 = 0; j0 < cnt; j0 += kWave) {
+    const int j = j0 + lane;
+    bool keep = false;
+    if (j < cnt) {
+      const ft8_result r = rs[j];
+      keep = r.ok != 0;
+      for (int q = 0; q < j && keep; ++q) {
+        if (!rs[q].ok) continue;
+        bool eq = true;
+        for (int b = 0; b < 10; ++b) eq = eq && rs[q].payload[b] == r.payload[b];
+        keep = !eq;
+      }
+      est[j].active = 0;
+    }
+    const uint64_t m = __ballot(keep);
+    if (keep) list[n + __popcll(m & ((1ull << lane) - 1ull))] = j;
+    n += __popcll(m);
+  }
+  if (lane == 0) list[a.cap] = n;
+}
 
 // REST = false: workgroup rec0 of a slot fits record rec0 (no loop: 108 VGPRs, four waves per
 // SIMD); REST = true: the records past kSubRecStride, kSubRecStride + rec0 + j kSubRestStride (a
@@ -87,26 +119,14 @@ __global__ __launch_bounds__(kSubThreads) void k_sub_est(SubLaunch a) {
   const int slot = (w % 8) + 8 * (j8 / kStride);
   const int rec0 = j8 % kStride;
   if (slot >= a.n_slots) return;
-  const int cnt = min(a.counts[slot], a.cap);
-  for (int rec = rec0 + (REST ? kSubRecStride : 0); rec < cnt; rec += kStride) {
+  const int32_t* list = a.list + (int64_t)slot * (a.cap + 1);
+  const int nfit = list[a.cap];
+  for (int i = rec0 + (REST ? kSubRecStride : 0); i < nfit; i += kStride) {
   __syncthreads();  // the previous record's LDS reads are done
+  const int rec = list[i];
   SubEst* est = reinterpret_cast<SubEst*>(a.est) + (int64_t)slot * a.cap + rec;
   const ft8_result* rs = a.res + (int64_t)slot * a.cap;
-  const ft8_result r = rs[rec];
-  // a failed record, or a payload an earlier record of the slot already carries: nothing to fit
-  bool dup = false;
-  for (int j = threadIdx.x; j < rec; j += kSubThreads) {
-    if (!rs[j].ok) continue;
-    bool eq = true;
-    for (int b = 0; b < 10; ++b) eq = eq && rs[j].payload[b] == r.payload[b];
-    dup = dup || eq;
-  }
-  dup = __syncthreads_or(dup);
-  if (!r.ok || dup) {
-    if (threadIdx.x == 0) est->active = 0;
-    if (!REST) break;
-    continue;
-  }
+  const ft8_result r = rs[rec];  // ok, and its payload's first record in the slot (k_sub_list)
   if (threadIdx.x < kWave) tx::encode_tones_wave(r.payload, threadIdx.x, s_tones);
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -519,9 +539,10 @@ hipError_t launch_sub_est(const SubLaunch& a, hipStream_t s) {
   if (a.n_slots <= 0 || a.n_samples <= 0) return hipSuccess;
   if (a.Q <= 0 || a.Q > kMaxQ || a.nsps % a.Q != 0 || a.hop <= 0 || a.nsps % a.hop != 0) return hipErrorInvalidValue;
   if (a.cap > 0) {
+    hipLaunchKernelGGL(k_sub_list, dim3(a.n_slots), dim3(kWave), 0, s, a);
     const unsigned grid = (unsigned)(((a.n_slots + 7) / 8) * 8 * (int64_t)kSubRecStride);
-    // the rest launch: 8 workgroups per slot, 2 700 near-empty ones at 334 slots (0.04 ms; at 64 per
-    // slot its 21 500 empty workgroups took 0.31 ms of wave launches)
+    // the rest launch: 8 workgroups per slot that exit at once unless the slot holds more than
+    // kSubRecStride fits
     const unsigned grid_rest = (unsigned)(((a.n_slots + 7) / 8) * 8 * (int64_t)kSubRestStride);
     const size_t mz = (size_t)tx::kSymbols * a.Q + 2 * (a.Q / (2 * (a.nsps / a.hop)) + 2);
     const size_t lds = std::max(mz * sizeof(float2), (size_t)(3 * a.nsps + 1) * sizeof(float));

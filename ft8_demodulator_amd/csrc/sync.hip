@@ -1067,7 +1067,8 @@ __global__ __launch_bounds__(kSelThreads) void k_topkc(SelectArgs a, int M, int 
   const float* sv = reinterpret_cast<const float*>(a.scores) + seg0 * kSegCols;
   const int N = a.N;
 
-  // ---- segment offsets (dense index of each segment's first passing score)
+  // ---- segment offsets (dense index of each segment's first passing score); the thread that owns
+  // a segment also stages its scores into s_val while they fit (only used when all of them do)
   int carry = 0;
   for (int g0 = 0; g0 < nsegs; g0 += kSelThreads) {
     const int sg = g0 + tid;
@@ -1075,7 +1076,21 @@ __global__ __launch_bounds__(kSelThreads) void k_topkc(SelectArgs a, int M, int 
     if (sg < nsegs) c = __popcll(mk[2 * sg]) + __popcll(mk[2 * sg + 1]);
     int ctot;
     const int ex = block_excl_sum(c, s_isum, &ctot);
-    if (sg < nsegs) s_off[sg] = carry + ex;
+    if (sg < nsegs) {
+      const int off = carry + ex;
+      s_off[sg] = off;
+      if (off + c <= V) {
+        const float* src = sv + (int64_t)sg * kSegCols;
+        for (int j0 = 0; j0 < c; j0 += kTkcRun) {
+          float v[kTkcRun];
+#pragma unroll
+          for (int u = 0; u < kTkcRun; ++u) v[u] = j0 + u < c ? src[j0 + u] : 0.0f;
+#pragma unroll
+          for (int u = 0; u < kTkcRun; ++u)
+            if (j0 + u < c) s_val[off + j0 + u] = v[u];
+        }
+      }
+    }
     carry += ctot;
   }
   const int total = carry;
@@ -1089,35 +1104,9 @@ __global__ __launch_bounds__(kSelThreads) void k_topkc(SelectArgs a, int M, int 
     s_cnt = 0;
   }
   __syncthreads();
+  // staged (every score fits s_val): the scan above copied them (the barrier after it orders
+  // the copies); else every pass reads them from HBM, one wave per segment
   const bool staged = total <= V;
-  if (staged) {
-    // thread t copies the dense run [t per, (t + 1) per): one search, then a walk over segments;
-    // kTkcRun loads in flight
-    const int per = (total + kSelThreads - 1) / kSelThreads;
-    const int d_lo = min(total, tid * per), d_hi = min(total, d_lo + per);
-    if (d_lo < d_hi) {
-      int sg = tkc_seg(s_off, nsegs, d_lo);
-      for (int b = d_lo; b < d_hi; b += kTkcRun) {
-        int64_t src[kTkcRun];
-#pragma unroll
-        for (int u = 0; u < kTkcRun; ++u) {
-          const int d = b + u;
-          src[u] = -1;
-          if (d < d_hi) {
-            while (s_off[sg + 1] <= d) ++sg;
-            src[u] = (int64_t)sg * kSegCols + (d - s_off[sg]);
-          }
-        }
-        float v[kTkcRun];
-#pragma unroll
-        for (int u = 0; u < kTkcRun; ++u) v[u] = src[u] >= 0 ? sv[src[u]] : 0.0f;
-#pragma unroll
-        for (int u = 0; u < kTkcRun; ++u)
-          if (b + u < d_hi) s_val[b + u] = v[u];
-      }
-    }
-    __syncthreads();
-  }
   // every passing score once: (dense index, value)
   auto visit = [&](auto&& fn) {
     if (staged) {
@@ -1227,14 +1216,40 @@ __global__ __launch_bounds__(kSelThreads) void k_topkc(SelectArgs a, int M, int 
     });
   }
   __syncthreads();
-  bitonic(s_key, s_sec, s_pay, nsort);
   if (tid == 0) {
     a.cand_count[slot] = nsel;
     a.warn[slot] = 0;
   }
+  // order by (-score, scan index).  Up to one item per thread: each thread counts the items that
+  // precede its own (LDS broadcast reads; the keys are distinct) and writes it at that rank --
+  // the 45 barrier rounds of a 512-item bitonic sort took a third of the kernel
+  const bool rank_sort = nsort <= kSelThreads;
+  int my_rank = 0;
+  if (rank_sort) {
+    if (tid < nsort) {
+      const double kt = s_key[tid];
+      const int st = s_sec[tid];
+      int j = 0;
+      for (; j + 4 <= nsort; j += 4) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const double kj = s_key[j + q];
+          my_rank += (kj < kt || (kj == kt && s_sec[j + q] < st)) ? 1 : 0;
+        }
+      }
+      for (; j < nsort; ++j) {
+        const double kj = s_key[j];
+        my_rank += (kj < kt || (kj == kt && s_sec[j] < st)) ? 1 : 0;
+      }
+    }
+  } else {
+    bitonic(s_key, s_sec, s_pay, nsort);
+  }
   // dense index -> grid position (row, column) through the segment's column-order mask
-  for (int i = tid; i < nsel; i += kSelThreads) {
-    const int d = s_pay[i];
+  for (int t_ = tid; t_ < (rank_sort ? nsort : nsel); t_ += kSelThreads) {
+    const int i = rank_sort ? my_rank : t_;
+    if (i >= nsel) continue;
+    const int d = s_pay[t_];
     const int sg = tkc_seg(s_off, nsegs, d);
     const int j = d - s_off[sg];
     const uint64_t e = mk[2 * sg], o = mk[2 * sg + 1];
@@ -1245,7 +1260,7 @@ __global__ __launch_bounds__(kSelThreads) void k_topkc(SelectArgs a, int M, int 
     const int row = sg / a.nseg;
     a.cand[((int64_t)slot * a.N + i) * 2 + 0] = a.t0 + row;
     a.cand[((int64_t)slot * a.N + i) * 2 + 1] = (sg - row * a.nseg) * kSegCols + col;
-    a.cand_score[(int64_t)slot * a.N + i] = -s_key[i];
+    a.cand_score[(int64_t)slot * a.N + i] = -s_key[t_];
   }
 }
 
