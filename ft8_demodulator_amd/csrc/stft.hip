@@ -235,7 +235,9 @@ struct FrameSrc {
 __device__ __forceinline__ int pidx(int i) { return i + (i >> 4); }
 
 // One Stockham stage of radix R.  MAXV = max complex values per thread (P <= 256 * MAXV).
-template <int R, int MAXV, bool FIRST, typename CT, typename Src>
+// HALF (first stage only): inputs j + r nbf with r >= R / 2 are the frame's zero padding (real
+// input, nperseg <= P), set as constants so the butterfly's first layer folds away
+template <int R, int MAXV, bool FIRST, typename CT, typename Src, bool HALF = false>
 __device__ __forceinline__ void stockham_stage(cplx<CT>* buf, int P, int Ns, const cplx<CT>* tw,
                                                const Src& src) {
   constexpr int MAXB = (MAXV + R - 1) / R;
@@ -248,7 +250,8 @@ __device__ __forceinline__ void stockham_stage(cplx<CT>* buf, int P, int Ns, con
     if (j < nbf) {
 #pragma unroll
       for (int r = 0; r < R; ++r) {
-        if constexpr (FIRST) v[b][r] = src(j + r * nbf);
+        if constexpr (FIRST && HALF) v[b][r] = r < R / 2 ? src(j + r * nbf) : cplx<CT>{(CT)0, (CT)0};
+        else if constexpr (FIRST) v[b][r] = src(j + r * nbf);
         else v[b][r] = buf[pidx(j + r * nbf)];
       }
     }
@@ -427,6 +430,55 @@ __global__ __launch_bounds__(kThreads, (MAXV <= 16 ? 2 : 1)) void k_stft(StftArg
     a.argmax[(int64_t)slot * nt + fi] = vi;
   }
 }
+
+// ---- k_stft_sp: the generic transform with a compile-time radix plan (round 4) -------------------
+// Real float32 / int16 input with the dB epilogue, for the plans of the reference's other
+// geometries: 20 kHz at bpt = sps = 2 (P = 3 200 = 16 x 8 x 5 x 5, the bundled recording's rate), 12 kHz
+// at bpt = sps = 10 (P = 9 600 = 16 x 8 x 15 x 5, the decode test's) and 6 kHz (P = 960 = 16 x 4 x 15).
+// k_stft's runtime radix switch keeps every case's registers live (206 VGPRs at P = 3 200, two
+// waves per SIMD; 439 at P = 9 600); with the stages fixed each holds only its own butterflies, and
+// the first stage's zero-padded half (nperseg <= P) is constant-folded.
+template <typename InT, int MAXV, int R0, int... Rs>
+__global__ __launch_bounds__(kThreads) void k_stft_sp(StftArgs a) {
+  FT8_RACE_PROLOGUE();
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  cplx<float>* buf = reinterpret_cast<cplx<float>*>(smem);
+  const int nt = a.nt_out;
+  const int r = (int)(blockIdx.x & 7) * a.per_xcd + (int)(blockIdx.x >> 3);  // XCD-aware, as k_stft
+  if (r >= nt * a.n_slots) return;
+  const int slot = r / nt;
+  const int fi = r - slot * nt;
+  const int frame = a.t_lo + fi;
+  const InT* xs = reinterpret_cast<const InT*>(a.samples) + (int64_t)slot * a.slot_stride + (int64_t)frame * a.hop;
+  FrameSrc<InT, false, float> src{xs, reinterpret_cast<const float*>(a.window), a.nperseg};
+  const cplx<float>* tw = reinterpret_cast<const cplx<float>*>(a.tw);
+  const int P = a.P;
+  stockham_stage<R0, MAXV, true, float, FrameSrc<InT, false, float>, true>(buf, P, 1, tw, src);
+  int Ns = R0;
+  ((stockham_stage<Rs, MAXV, false>(buf, P, Ns, tw, src), Ns *= Rs), ...);
+
+  const float scale = (float)a.scale;
+  const cplx<float>* post = reinterpret_cast<const cplx<float>*>(a.post);
+  constexpr float kDb = 3.0102999566398119521f;  // 10 log10(v) = (10 log10 2) log2(v), v >= 1e-12
+  float* out = reinterpret_cast<float*>(a.out) + ((int64_t)slot * a.nt_out + fi) * a.nf_out;
+  for (int i = threadIdx.x; i < a.nf_out; i += kThreads) {
+    const int k = a.f_lo + i;
+    const int kk = (k <= P) ? k : a.nfft - k;  // real signal: X[N-k] = conj X[k]
+    const cplx<float> A = buf[pidx(kk == P ? 0 : kk)];
+    const cplx<float> Bc = buf[pidx(kk == 0 ? 0 : P - kk)];
+    const cplx<float> B = {Bc.x, -Bc.y};
+    const cplx<float> sm = cadd(A, B), d = csub(A, B);
+    const cplx<float> wd = cmul(post[kk], d);
+    const cplx<float> X = {0.5f * (sm.x + wd.y), 0.5f * (sm.y - wd.x)};  // X = s/2 - i wd/2
+    out[i] = kDb * __builtin_amdgcn_logf(1e-12f + (X.x * X.x + X.y * X.y) * scale);
+  }
+}
+
+// the static plans k_stft_sp is built for: {P, radices...}
+struct SpPlan {
+  int P, n, r[5];
+};
+constexpr SpPlan kSpPlans[] = {{3200, 4, {16, 8, 5, 5}}, {9600, 4, {16, 8, 15, 5}}, {960, 3, {16, 4, 15}}};
 
 // ---- k_stftc3840: complex input, nfft = 3840, nperseg = 1920, hop = 240 M (M in 1, 2, 4, 8) -----
 // The beacon receiver's geometry (12 kHz complex baseband, frequency_correction.py; the reference
@@ -886,6 +938,18 @@ hipError_t launch_t(const StftLaunch& L, const StftArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(kern, grid, dim3(kThreads), lds, s, a);
     return hipGetLastError();
   };
+  if constexpr (!CPLX && sizeof(CT) == 4) {
+    // a static plan for the reference's other real-input geometries (dB rows, nperseg <= P)
+    auto plan_is = [&](const SpPlan& q) {
+      if (a.P != q.P || a.nstages != q.n || a.argmax != nullptr || a.nperseg > a.P) return false;
+      for (int i = 0; i < q.n; ++i)
+        if (a.radix[i] != q.r[i]) return false;
+      return true;
+    };
+    if (plan_is(kSpPlans[0])) return go(k_stft_sp<InT, 13, 16, 8, 5, 5>);
+    if (plan_is(kSpPlans[1])) return go(k_stft_sp<InT, 38, 16, 8, 15, 5>);
+    if (plan_is(kSpPlans[2])) return go(k_stft_sp<InT, 4, 16, 4, 15>);
+  }
   if (a.P <= kThreads * 8) return go(k_stft<InT, CPLX, CT, 8>);
   // P <= 3840 (3840 = 16 x 16 x 15: one butterfly per thread per stage) keeps half the registers
   // of the P <= 4096 variant, whose radix-15 stage would hold two butterflies per thread
