@@ -526,7 +526,45 @@ __device__ void bitonic(double* key, int* sec, int* pay, int n) {
   }
 }
 
-// block-wide maximum of a u64 key
+// (key asc, sec asc) order of n items in LDS, in place.  Up to one item per thread (n <= 1024): each
+// thread counts the items that precede its own (LDS broadcast reads; sec is distinct, so ranks are
+// too) and writes it at that rank -- two barriers instead of the bitonic network's 45 rounds for a
+// few hundred items (round 4); larger sets take the bitonic sort.
+__device__ void sort_kv(double* key, int* sec, int* pay, int n) {
+  if (n > kSelThreads) {
+    bitonic(key, sec, pay, n);
+    return;
+  }
+  const int t = threadIdx.x;
+  double kt = 0.0;
+  int st = 0, pt = 0, rank = 0;
+  if (t < n) {
+    kt = key[t];
+    st = sec[t];
+    pt = pay[t];
+    int j = 0;
+    for (; j + 4 <= n; j += 4) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const double kj = key[j + q];
+        rank += (kj < kt || (kj == kt && sec[j + q] < st)) ? 1 : 0;
+      }
+    }
+    for (; j < n; ++j) {
+      const double kj = key[j];
+      rank += (kj < kt || (kj == kt && sec[j] < st)) ? 1 : 0;
+    }
+  }
+  __syncthreads();
+  if (t < n) {
+    key[rank] = kt;
+    sec[rank] = st;
+    pay[rank] = pt;
+  }
+  __syncthreads();
+}
+
+// block-wide maximum of a u64 key// block-wide maximum of a u64 key
 __device__ unsigned long long block_max_u64(unsigned long long v, unsigned long long* sh) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
@@ -754,7 +792,7 @@ __global__ __launch_bounds__(kSelThreads) void k_select(SelectArgs a) {
   __syncthreads();
 
   // order: score descending; equal scores keep the reference's heap-array order (below)
-  bitonic(s_key, s_sec, s_pay, nsel);
+  sort_kv(s_key, s_sec, s_pay, nsel);
   for (int i = threadIdx.x; i + 1 < nsel; i += kSelThreads)
     if (s_key[i] == s_key[i + 1]) s_flag[0] = 1;
   __syncthreads();
@@ -843,7 +881,7 @@ __global__ __launch_bounds__(kSelThreads) void k_select(SelectArgs a) {
       // sorted(key=-score) is stable on heap-array order: secondary key = heap position
       for (int i = threadIdx.x; i < nsel; i += kSelThreads) { s_pay[i] = s_sec[i]; s_sec[i] = i; }
       __syncthreads();
-      bitonic(s_key, s_sec, s_pay, nsel);
+      sort_kv(s_key, s_sec, s_pay, nsel);
     }
   }
   if (threadIdx.x == 0) {
@@ -1004,7 +1042,7 @@ __global__ __launch_bounds__(kSelThreads) void k_topk(SelectArgs a) {
     }
   }
   __syncthreads();
-  bitonic(s_key, s_sec, s_pay, nsort);
+  sort_kv(s_key, s_sec, s_pay, nsort);
   if (threadIdx.x == 0) {
     a.cand_count[slot] = nsel;
     a.warn[slot] = 0;
