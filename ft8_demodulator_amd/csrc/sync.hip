@@ -392,6 +392,14 @@ hipError_t launch_score2(const SyncLaunch& L, const ScoreArgs& a0, hipStream_t s
   a.n_ctiles = (L.NF + kS2TW - 1) / kS2TW;
   const size_t lds = sizeof(float) * G::kFloats;
   static_assert(sizeof(float) * S2Geom<4, 4>::kFloats <= 64 * 1024, "one band fits the default LDS limit");
+  static_assert(sizeof(float) * G::kFloats <= 160 * 1024, "one band fits the CU's LDS");
+  if constexpr (sizeof(float) * G::kFloats > 64 * 1024) {
+    // bpt = sps = 10 (the reference decode test's geometry): a band is 102 rows x 200 columns,
+    // 82 KB -- one workgroup per CU, still far from the generic kernel's uncached row reads
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k_score2<BPT, SPS, COMPACT>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
   const int groups = (L.n_slots + 7) / 8;
   const int64_t blocks = (int64_t)groups * 8 * a.n_bands * a.n_ctiles;
   hipLaunchKernelGGL((k_score2<BPT, SPS, COMPACT>), dim3((unsigned)blocks), dim3(kS2Threads), lds, s, a);
@@ -399,7 +407,7 @@ hipError_t launch_score2(const SyncLaunch& L, const ScoreArgs& a0, hipStream_t s
 }
 
 bool score2_path(const SyncLaunch& L) {
-  return !L.wf_f64 && L.bpt == L.sps && L.bpt >= 1 && L.bpt <= 4;
+  return !L.wf_f64 && L.bpt == L.sps && ((L.bpt >= 1 && L.bpt <= 4) || L.bpt == 10);
 }
 template <int B>
 hipError_t launch_score2_any(const SyncLaunch& L, const ScoreArgs& a, hipStream_t s) {
@@ -434,6 +442,7 @@ hipError_t launch_score_t(const SyncLaunch& L, hipStream_t s) {
         case 2: return launch_score2_any<2>(L, a, s);
         case 3: return launch_score2_any<3>(L, a, s);
         case 4: return launch_score2_any<4>(L, a, s);
+        case 10: return launch_score2_any<10>(L, a, s);
         default: break;
       }
     }
