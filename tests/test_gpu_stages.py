@@ -25,6 +25,34 @@ def test_score_grid_bit_exact(golden, gpu):
         assert np.array_equal(g.view(np.uint8), ref.view(np.uint8)), c["name"]
 
 
+def test_score_grid_bpt10_bit_exact(gpu, oracle):
+    """k_score2 at bins_per_tone = steps_per_symbol = 10 (round 4; the reference decode test's
+    geometry, test_spectrogram_analyse.py:128-163): full grid bit-exact against the oracle (which
+    follows ft8_decode.py:47-100), and the compact-layout selections (reference heap and top-k)
+    equal the full-grid ones, on a waterfall with strong tones over noise."""
+    from ft8_demodulator_amd import _device, ft8_score_grid
+    rng = np.random.default_rng(1010)
+    F, T = 1200, 940   # 10x oversampled: 120 tones x 94 blocks
+    mag = (rng.standard_normal((F, T)) * 3.0 - 70.0).astype(np.float32)
+    mag[300:310, 100:890] += 25.0
+    mag[700:705, 40:600] += 18.0
+    wf = _wf(mag, 10, 10)
+    g = ft8_score_grid(wf)
+    ref = oracle.score_grid(mag, 10, 10)
+    assert g.shape == ref.shape and g.dtype == ref.dtype
+    assert np.array_equal(g.view(np.uint8), ref.view(np.uint8))
+    for N, ms, flags in ((300, 2, 0), (1000, 0.5, 0), (300, 2, 1), (4096, -100, 1)):
+        compact, _, w1 = _device.sync_select(wf, N, ms, flags=flags)
+        full, _, w2 = _device.sync_select(wf, N, ms, want_grid=True, flags=flags)
+        assert compact == full and w1 == w2, (N, ms, flags)
+        if flags == 0:
+            idx, sc, tie = oracle.select(ref, N, ms)
+        else:
+            idx, sc = oracle.select_topk(ref, N, ms)
+        NF = ref.shape[1]
+        assert [(a, b) for a, b, _ in compact] == [(int(i // NF) - 100, int(i % NF)) for i in idx], (N, ms, flags)
+
+
 def test_candidates_exact(golden, gpu):
     from ft8_demodulator_amd import _device, ft8_find_candidates
     meta, arr = golden

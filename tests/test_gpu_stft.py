@@ -42,7 +42,10 @@ ST, P38, CZ, DFT = 0, 1, 2, 3  # ft8_stft_method: Stockham, packed 3840, chirp-z
     (11025, 3, 2, False, np.float32, ST),    # nfft 5292 = 2^2 3^3 7^2 ... P = 2646 = 2 3^3 7^2: FFT path
     (9973, 1, 2, False, np.float32, CZ),     # prime-ish rate: nfft 1595 = 5 x 11 x 29, odd real
     (9973, 2, 2, True, np.complex64, CZ),    # nfft 3191, a prime
-    (12000, 10, 10, False, np.float32, ST),  # nfft 19200: the 40-values-per-thread LDS FFT (P 9600)
+    (12000, 10, 10, False, np.float32, ST),  # nfft 19200: k_stft_sp's 16 x 8 x 15 x 5 plan (P 9600)
+    (20000, 2, 2, False, np.float32, ST),    # the bundled recording's rate: k_stft_sp, 16 x 8 x 5 x 5 (P 3200)
+    (6000, 2, 2, False, np.float32, ST),     # the reference decode test's 6 kHz: k_stft_sp, 16 x 4 x 15 (P 960)
+    (20000, 2, 2, False, np.float64, ST),    # float64 at the same plan: the generic k_stft
     (12000, 5, 2, True, np.complex64, ST),   # complex nfft 9600 in (8192, 10240]: the same variant
     (12000, 2, 2, False, np.float32, P38),   # the production geometry
     (12000, 2, 2, True, np.complex64, ST),   # complex input, nfft 3840: k_stftc3840 dB epilogue (hop 960)
