@@ -468,7 +468,7 @@ def geometry_legs(dev, reps=5):
                         "K=300, min_score=2, 20 iterations",
             "slots_per_s": n / dt, "ms_per_batch": dt * 1e3, "decodes_per_batch": decodes,
             "stft_method": {0: "stockham", 1: "packed3840", 2: "chirp-z", 3: "direct DFT"}.get(method, method),
-            "score_kernel": "k_score2" if bpt == sps and bpt <= 4 else "k_score",
+            "score_kernel": "k_score2" if bpt == sps and (bpt <= 4 or bpt == 10) else "k_score",
             "stages_ms": stages,
             "roofline_stft": {"bound": "hbm", "bytes_per_launch": stft_b, "launch_ms": stages["stft"],
                               "achieved": stft_b / (stages["stft"] * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
