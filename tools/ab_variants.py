@@ -21,14 +21,23 @@ for _ in range(30): out, cnt = dec.run(x)
 torch.cuda.synchronize()
 dt = (time.perf_counter() - t0) / 30
 tm = {}
-for st in ("stft", "score", "llr", "bp"):
+for st in ("stft", "score", "select", "llr", "bp"):
     ctx.set_timing(True, stages=[st]); ctx.timing(reset=True)
     for _ in range(8): dec.run(x)
     torch.cuda.synchronize()
     ctx.set_timing(False)
     tm[st] = ctx.timing(reset=True)[st]
+# the top-k selection (k_topkc) on the same batch
+dk = SlotDecoder(12000, 2, 2, 300, 2, 20, flags=1)
+for _ in range(3): dk.run(x)
+ctx.set_timing(True, stages=["select"]); ctx.timing(reset=True)
+for _ in range(8): dk.run(x)
+torch.cuda.synchronize()
+ctx.set_timing(False)
+tk = ctx.timing(reset=True)["select"]
 print(json.dumps({"lib": os.environ["FT8HIP_LIB"], "ms_step": dt * 1e3, "decodes": int(cnt.sum()),
-                  "stages": {k: v[0] / max(v[1], 1) for k, v in tm.items() if v[1]}}))
+                  "stages": {k: v[0] / max(v[1], 1) for k, v in tm.items() if v[1]},
+                  "topk_select": tk[0] / max(tk[1], 1)}))
 '''
 
 
