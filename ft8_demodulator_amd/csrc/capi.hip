@@ -63,6 +63,7 @@ struct ft8_ctx {
   std::vector<unsigned long long> work_base;
   // FT8_FLAG_SUBTRACT: residual samples, per-record fits, pass-1 / pass-2 records
   DevBuf residual, sub_est, sub_list, out1, counts1, out2, counts2;
+  DevBuf screen;  // complex128 argmax STFT: [count][frames] uncertain-frame list (stft.hip)
   int sub_slots = 0, sub_cap = 0;  // shape of the fits in sub_est (ft8_subtract_fits)
   // cumulative GFSK pulse of the transmit chain for one nsps (double and float)
   int gfsk_nsps = 0;
@@ -862,6 +863,12 @@ int stft_argmax_core(ft8_ctx* c, const void* x, int dtype, int64_t n_samples, in
   L.window = w->w;
   L.scale = w->scale;
   L.argmax = idx;
+  if (dtype == FT8_C128 && !L.plan.dft && !L.plan.blue && g.nfft == 3840 && g.nperseg == 1920) {
+    const size_t frames = (size_t)n_slots * (size_t)(p->t_hi - p->t_lo);
+    if ((rc = ensure(c, c->screen, sizeof(int32_t) * (frames + 1)))) return rc;
+    L.screen_count = (int32_t*)c->screen.p;
+    L.screen_list = L.screen_count + 1;
+  }
   StageTimer tm(c, 8, s);
   hipError_t e = launch_stft(L, s);
   tm.done();
@@ -982,7 +989,7 @@ int ft8_destroy(ft8_ctx* c) {
   {
     DeviceGuard dg(c->device);
     for (auto* b : {&c->wf, &c->scores, &c->smask, &c->cand, &c->cand_score, &c->cand_count, &c->warn, &c->rowsum,
-                    &c->res_all, &c->work, &c->stats, &c->llr, &c->tie, &c->residual, &c->sub_est, &c->sub_list, &c->out1,
+                    &c->res_all, &c->work, &c->stats, &c->llr, &c->tie, &c->residual, &c->sub_est, &c->sub_list, &c->screen, &c->out1,
                     &c->counts1, &c->out2, &c->counts2, &c->gfsk_P, &c->gfsk_Pf, &c->drift_idx, &c->drift_tmpl})
       if (b->p) (void)hipFree(b->p);
     for (auto& p : c->plans) {

@@ -93,6 +93,8 @@ struct StftLaunch {
   void* out;               // float or double [n_slots][t_hi-t_lo][f_hi-f_lo]
   int32_t* argmax;         // non-null: write per-frame argmax over the kept bins instead of `out`
                            // (a direct-DFT plan then writes the dB rows to `out` first)
+  int32_t* screen_list;    // non-null (complex128 argmax, 3840-point geometry): float32 screening
+  int32_t* screen_count;   // with the uncertain frames listed here and redone in float64
   FftPlan plan;
 };
 hipError_t launch_stft(const StftLaunch& a, hipStream_t s);

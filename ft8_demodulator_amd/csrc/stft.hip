@@ -304,6 +304,10 @@ struct StftArgs {
   const void* post;
   int32_t* argmax;  // non-null: per-frame argmax of the kept dB row instead of the row itself
   int n_slots, per_xcd;
+  // k_stftc3840 screening (complex128 argmax): frames whose float32 argmax is not certain are
+  // appended to list[0 .. *list_count) as slot * nt_out + frame, and re-done in float64
+  int32_t* list;
+  int32_t* list_count;
 };
 
 // np.argmax order: the first NaN wins, else the largest value, ties to the lower index
@@ -535,7 +539,10 @@ __device__ __forceinline__ cplx<CT> load_c(const InT* x, int64_t n) {
 
 // AMAX: the argmax epilogue (its own instantiation: a kernel carrying both epilogues is allocated
 // for the dB one's fifteen inlined float64 log10)
-template <typename InT, typename CT, int M, bool AMAX>
+// MODE: 0 dB rows, 1 argmax (level_better), 2 float32 screening argmax (CT = float; uncertain
+// frames listed), 3 the listed frames again in float64 (CT = double), one frame at a time
+constexpr int kScreenKappa = 256;  // FFT error bound factor of the screening test (see below)
+template <typename InT, typename CT, int M, int MODE>
 __global__ __launch_bounds__(kC38Threads, 2) void k_stftc3840(StftArgs a) {
   FT8_RACE_PROLOGUE();
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -548,9 +555,11 @@ __global__ __launch_bounds__(kC38Threads, 2) void k_stftc3840(StftArgs a) {
   const int nt = a.nt_out;
   const int chunks = (nt + kC38Chunk - 1) / kC38Chunk;
   const int rr = (int)(blockIdx.x & 7) * a.per_xcd + (int)(blockIdx.x >> 3);
-  if (rr >= chunks * a.n_slots) return;
-  const int slot = rr / chunks, c = rr - slot * chunks;
-  const int f_begin = c * kC38Chunk, f_end = min(nt, f_begin + kC38Chunk);
+  if (MODE != 3 && rr >= chunks * a.n_slots) return;
+  if (MODE == 3 && (int)blockIdx.x >= *a.list_count) return;
+  int slot = rr / chunks;
+  const int c = rr - slot * chunks;
+  int f_begin = c * kC38Chunk, f_end = min(nt, f_begin + kC38Chunk);
   const cplx<CT>* tw = reinterpret_cast<const cplx<CT>*>(a.tw);  // W_3840^m
   const CT* win = reinterpret_cast<const CT*>(a.window);
   const bool s1 = t < 240;
@@ -559,6 +568,20 @@ __global__ __launch_bounds__(kC38Threads, 2) void k_stftc3840(StftArgs a) {
   // twiddle seeds: stage 2 W_256^k = W_3840^(15 k) (k = t % 16), stage 3 W_3840^t; their powers are
   // formed by complex recurrence each frame (relative error ~15 ulp, far inside the tolerances)
   cplx<CT> s2 = tw[15 * (t & 15)], s3 = tw[t];
+  const CT scale = (CT)a.scale;
+  constexpr bool amax = MODE != 0;
+  const int k_lo = a.f_lo, k_hi = a.f_lo + a.nf_out;
+  // MODE 3: workgroup l takes listed frames l, l + gridDim, ...: one frame at a time, its 8 raw
+  // samples per thread loaded afresh
+  const int n_list = MODE == 3 ? *a.list_count : 0;
+  for (int l = blockIdx.x;; l += gridDim.x) {
+  if constexpr (MODE == 3) {
+    if (l >= n_list) break;
+    const int code = a.list[l];
+    slot = code / nt;
+    f_begin = code - slot * nt;
+    f_end = f_begin + 1;
+  }
   const InT* xs = reinterpret_cast<const InT*>(a.samples) + (int64_t)slot * a.slot_stride * 2;
   cplx<CT> raw[8];
   {
@@ -566,9 +589,6 @@ __global__ __launch_bounds__(kC38Threads, 2) void k_stftc3840(StftArgs a) {
 #pragma unroll
     for (int r = 0; r < 8; ++r) raw[r] = s1 ? load_c<InT, CT>(xs, base + t + 240 * r) : cplx<CT>{(CT)0, (CT)0};
   }
-  const CT scale = (CT)a.scale;
-  constexpr bool amax = AMAX;
-  const int k_lo = a.f_lo, k_hi = a.f_lo + a.nf_out;
   for (int f = f_begin; f < f_end; ++f) {
     // re-opaque the seeds so the per-frame twiddle powers are not hoisted into ~60 live registers
     if constexpr (sizeof(CT) == 8) {
@@ -643,6 +663,77 @@ __global__ __launch_bounds__(kC38Threads, 2) void k_stftc3840(StftArgs a) {
           else out[k - k_lo] = 10.0 * log10(lv[r]);
         }
       }
+    } else if constexpr (MODE == 2) {
+      // float32 screening: the two largest kept levels (first index on equal ones) and the total
+      // energy of the frame's spectrum.  An FFT's rounding error in any one bin is bounded by a
+      // small multiple of u log2(N) times the spectrum's L2 norm (u = 2^-24), so with
+      // delta = kappa u sqrt(E) (kappa = 256, over ten times the analytic constant with the
+      // twiddle recurrences' ~15 ulp) the float64 transform orders bins i1 and i2 the same way
+      // whenever L1 - L2 > 2 (2 sqrt(L1) delta + delta^2) + 8 u L1; the float64 argmax then is i1.
+      // Every other frame is listed and transformed again in float64 (MODE 3).
+      float l1 = -INFINITY, l2 = -INFINITY, es = 0.0f;
+      int i1 = 0x7fffffff;
+#pragma unroll
+      for (int r = 0; r < 15; ++r) {
+        const int k = t + 256 * r;
+        es += lv[r] - 1e-12f;
+        if (k >= k_lo && k < k_hi) {
+          if (lv[r] > l1 || (lv[r] == l1 && k < i1)) {
+            l2 = l1;
+            l1 = lv[r];
+            i1 = k;
+          } else if (lv[r] > l2) {
+            l2 = lv[r];
+          }
+        }
+      }
+#pragma unroll
+      for (int off = kWave / 2; off > 0; off >>= 1) {
+        const float o1 = __shfl_xor(l1, off), o2 = __shfl_xor(l2, off);
+        const int oi = __shfl_xor(i1, off);
+        es += __shfl_xor(es, off);
+        if (o1 > l1 || (o1 == l1 && oi < i1)) {
+          l2 = fmaxf(l1, o2);
+          l1 = o1;
+          i1 = oi;
+        } else {
+          l2 = fmaxf(l2, o1);
+        }
+      }
+      // the 16 words before the window: l1 [0, 4), si's indices [4, 8), l2 [8, 12), es [12, 16)
+      float* s_l = reinterpret_cast<float*>(sv);
+      if ((t & (kWave - 1)) == 0) {
+        s_l[w_id] = l1;
+        si[w_id] = i1;
+        s_l[8 + w_id] = l2;
+        s_l[12 + w_id] = es;
+      }
+      __syncthreads();
+      if (t == 0) {
+        double e_tot = s_l[12];
+        for (int q = 1; q < kC38Threads / kWave; ++q) {
+          const float o1 = s_l[q], o2 = s_l[8 + q];
+          const int oi = si[q];
+          e_tot += s_l[12 + q];
+          if (o1 > l1 || (o1 == l1 && oi < i1)) {
+            l2 = fmaxf(l1, o2);
+            l1 = o1;
+            i1 = oi;
+          } else {
+            l2 = fmaxf(l2, o1);
+          }
+        }
+        const double u = 0x1p-24;
+        const double delta = kScreenKappa * u * sqrt(fmax(e_tot, 0.0) * 1.0001);
+        const double need = 2.0 * (2.0 * sqrt((double)l1) * delta + delta * delta) + 8.0 * u * (double)l1;
+        const int64_t fi = (int64_t)slot * nt + f;
+        if ((double)l1 - (double)l2 > need && l1 == l1) {
+          a.argmax[fi] = i1 - k_lo;
+        } else {
+          const int pos = atomicAdd(a.list_count, 1);
+          a.list[pos] = (int)fi;
+        }
+      }
     } else {
       // one-pass argmax of the dB row on the levels (level_better)
       CT vm = -__builtin_huge_val();
@@ -674,6 +765,8 @@ __global__ __launch_bounds__(kC38Threads, 2) void k_stftc3840(StftArgs a) {
       for (int q = 0; q < M; ++q) raw[8 - M + q] = nx[q];
     }
   }
+  if constexpr (MODE != 3) break;  // a run of frames: one pass of the outer loop
+  }
 }
 
 template <typename InT, typename CT>
@@ -692,7 +785,7 @@ hipError_t launch_c3840(const StftLaunch& L, StftArgs a, hipStream_t s) {
     return hipGetLastError();
   };
   auto go_m = [&](auto am) {
-    constexpr bool AM = decltype(am)::value;
+    constexpr int AM = decltype(am)::value;
     switch (L.hop) {
       case 240: return go(k_stftc3840<InT, CT, 1, AM>);
       case 480: return go(k_stftc3840<InT, CT, 2, AM>);
@@ -700,7 +793,48 @@ hipError_t launch_c3840(const StftLaunch& L, StftArgs a, hipStream_t s) {
       default: return go(k_stftc3840<InT, CT, 8, AM>);
     }
   };
-  return a.argmax != nullptr ? go_m(std::true_type{}) : go_m(std::false_type{});
+  if (a.argmax == nullptr) return go_m(std::integral_constant<int, 0>{});
+  return go_m(std::integral_constant<int, 1>{});
+}
+
+// complex128 argmax in two steps: the float32 transform decides every frame whose argmax the
+// float32 error bound settles (MODE 2), the float64 transform redoes the others (MODE 3, a
+// persistent grid over the device-side list; typically a few percent of the frames)
+hipError_t launch_c3840_screened(const StftLaunch& L, StftArgs a, hipStream_t s) {
+  a.list = L.screen_list;
+  a.list_count = L.screen_count;
+  hipError_t e = hipMemsetAsync(L.screen_count, 0, sizeof(int32_t), s);
+  if (e != hipSuccess) return e;
+  const int chunks = (a.nt_out + kC38Chunk - 1) / kC38Chunk;
+  a.per_xcd = (int)(((int64_t)chunks * L.n_slots + 7) / 8);
+  const size_t lds32 = (size_t)(kC38P + kC38P / 16 + 1) * sizeof(cplx<float>) + 16 * sizeof(float) + 1920 * sizeof(float);
+  const size_t lds64 = (size_t)(kC38P + kC38P / 16 + 1) * sizeof(cplx<double>) + 16 * sizeof(double) + 1920 * sizeof(double);
+  auto go = [&](auto kern, dim3 grid, size_t lds) {
+    if (lds > 64 * 1024) {
+      hipError_t e2 = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                          (int)lds);
+      if (e2 != hipSuccess) return e2;
+    }
+    hipLaunchKernelGGL(kern, grid, dim3(kC38Threads), lds, s, a);
+    return hipGetLastError();
+  };
+  const dim3 g1((unsigned)(8 * a.per_xcd));
+  const int64_t frames = (int64_t)a.nt_out * L.n_slots;
+  const dim3 g2((unsigned)std::min<int64_t>(frames, 512));  // two float64 workgroups per CU
+  switch (L.hop) {
+    case 240:
+      if ((e = go(k_stftc3840<double, float, 1, 2>, g1, lds32)) != hipSuccess) return e;
+      return go(k_stftc3840<double, double, 1, 3>, g2, lds64);
+    case 480:
+      if ((e = go(k_stftc3840<double, float, 2, 2>, g1, lds32)) != hipSuccess) return e;
+      return go(k_stftc3840<double, double, 2, 3>, g2, lds64);
+    case 960:
+      if ((e = go(k_stftc3840<double, float, 4, 2>, g1, lds32)) != hipSuccess) return e;
+      return go(k_stftc3840<double, double, 4, 3>, g2, lds64);
+    default:
+      if ((e = go(k_stftc3840<double, float, 8, 2>, g1, lds32)) != hipSuccess) return e;
+      return go(k_stftc3840<double, double, 8, 3>, g2, lds64);
+  }
 }
 
 // ---- k_stft_dft: direct DFT for lengths the FFT plans cannot take ---------------------------
@@ -1014,6 +1148,7 @@ hipError_t launch_stft(const StftLaunch& L, hipStream_t s) {
   // complex input in the beacon receiver's geometry (12 kHz: nfft 3840, nperseg 1920, hop 240 M)
   if ((L.dtype == FT8_C64 || L.dtype == FT8_C128) && L.nfft == kC38P && L.nperseg == 1920 && a.P == kC38P &&
       (L.hop == 240 || L.hop == 480 || L.hop == 960 || L.hop == 1920)) {
+    if (L.dtype == FT8_C128 && L.argmax && L.screen_list) return launch_c3840_screened(L, a, s);
     if (L.dtype == FT8_C128) return launch_c3840<double, double>(L, a, s);
     return launch_c3840<float, float>(L, a, s);
   }

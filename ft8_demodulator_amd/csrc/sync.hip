@@ -535,45 +535,69 @@ __device__ void bitonic(double* key, int* sec, int* pay, int n) {
   }
 }
 
-// (key asc, sec asc) order of n items in LDS, in place.  Up to one item per thread (n <= 1024): each
-// thread counts the items that precede its own (LDS broadcast reads; sec is distinct, so ranks are
-// too) and writes it at that rank -- two barriers instead of the bitonic network's 45 rounds for a
-// few hundred items (round 4); larger sets take the bitonic sort.
+// (key asc, sec asc) order of n items in LDS, in place (sec is distinct).  Up to 1024 items: one
+// per thread in registers, a bitonic network whose exchanges of partners less than 64 apart are
+// wave shuffles and only the six (at 512 items) farther ones go through LDS with barriers -- the
+// LDS network (bitonic) takes a barrier for every one of its 45 rounds.  Larger sets take bitonic.
+__device__ __forceinline__ bool kv_less(double ka, int sa, double kb, int sb) {
+  return ka < kb || (ka == kb && sa < sb);
+}
 __device__ void sort_kv(double* key, int* sec, int* pay, int n) {
   if (n > kSelThreads) {
     bitonic(key, sec, pay, n);
     return;
   }
+  int m = 1;
+  while (m < n) m <<= 1;
   const int t = threadIdx.x;
-  double kt = 0.0;
-  int st = 0, pt = 0, rank = 0;
+  double k_ = INFINITY;
+  int s_ = 0x7fffffff, p_ = -1;
   if (t < n) {
-    kt = key[t];
-    st = sec[t];
-    pt = pay[t];
-    int j = 0;
-    for (; j + 4 <= n; j += 4) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const double kj = key[j + q];
-        rank += (kj < kt || (kj == kt && sec[j + q] < st)) ? 1 : 0;
+    k_ = key[t];
+    s_ = sec[t];
+    p_ = pay[t];
+  }
+  for (int k = 2; k <= m; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      double ko;
+      int so, po;
+      if (j >= kWave) {
+        __syncthreads();  // every earlier read of the arrays is done
+        if (t < m) {
+          key[t] = k_;
+          sec[t] = s_;
+          pay[t] = p_;
+        }
+        __syncthreads();
+        const int q = t ^ j;
+        ko = t < m ? key[q] : k_;
+        so = t < m ? sec[q] : s_;
+        po = t < m ? pay[q] : p_;
+      } else {
+        ko = __shfl_xor(k_, j);
+        so = __shfl_xor(s_, j);
+        po = __shfl_xor(p_, j);
       }
-    }
-    for (; j < n; ++j) {
-      const double kj = key[j];
-      rank += (kj < kt || (kj == kt && sec[j] < st)) ? 1 : 0;
+      // ascending blocks where (t & k) == 0; the lower index of a pair keeps the smaller there
+      const bool up = (t & k) == 0, lower = (t & j) == 0;
+      const bool take = (up == lower) ? kv_less(ko, so, k_, s_) : kv_less(k_, s_, ko, so);
+      if (take && t < m) {
+        k_ = ko;
+        s_ = so;
+        p_ = po;
+      }
     }
   }
   __syncthreads();
   if (t < n) {
-    key[rank] = kt;
-    sec[rank] = st;
-    pay[rank] = pt;
+    key[t] = k_;
+    sec[t] = s_;
+    pay[t] = p_;
   }
   __syncthreads();
 }
 
-// block-wide maximum of a u64 key// block-wide maximum of a u64 key
+// block-wide maximum of a u64 key
 __device__ unsigned long long block_max_u64(unsigned long long v, unsigned long long* sh) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
@@ -1267,36 +1291,12 @@ __global__ __launch_bounds__(kSelThreads) void k_topkc(SelectArgs a, int M, int 
     a.cand_count[slot] = nsel;
     a.warn[slot] = 0;
   }
-  // order by (-score, scan index).  Up to one item per thread: each thread counts the items that
-  // precede its own (LDS broadcast reads; the keys are distinct) and writes it at that rank --
-  // the 45 barrier rounds of a 512-item bitonic sort took a third of the kernel
-  const bool rank_sort = nsort <= kSelThreads;
-  int my_rank = 0;
-  if (rank_sort) {
-    if (tid < nsort) {
-      const double kt = s_key[tid];
-      const int st = s_sec[tid];
-      int j = 0;
-      for (; j + 4 <= nsort; j += 4) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const double kj = s_key[j + q];
-          my_rank += (kj < kt || (kj == kt && s_sec[j + q] < st)) ? 1 : 0;
-        }
-      }
-      for (; j < nsort; ++j) {
-        const double kj = s_key[j];
-        my_rank += (kj < kt || (kj == kt && s_sec[j] < st)) ? 1 : 0;
-      }
-    }
-  } else {
-    bitonic(s_key, s_sec, s_pay, nsort);
-  }
+  // order by (-score, scan index) (sort_kv: a register network for up to 1024 items)
+  sort_kv(s_key, s_sec, s_pay, nsort);
   // dense index -> grid position (row, column) through the segment's column-order mask
-  for (int t_ = tid; t_ < (rank_sort ? nsort : nsel); t_ += kSelThreads) {
-    const int i = rank_sort ? my_rank : t_;
-    if (i >= nsel) continue;
-    const int d = s_pay[t_];
+  for (int i = tid; i < nsel; i += kSelThreads) {
+    const int t_ = i;
+    const int d = s_pay[i];
     const int sg = tkc_seg(s_off, nsegs, d);
     const int j = d - s_off[sg];
     const uint64_t e = mk[2 * sg], o = mk[2 * sg + 1];

@@ -291,6 +291,43 @@ def test_subtract_int16_and_batch_consistency(gpu):
         SlotDecoder(**kw).records(x.double(), _lib.FT8_F64)
 
 
+def test_subtract_mixed_batch_with_silent_and_dense_slots(gpu):
+    """k_sub_list / k_sub_est / k_sub_apply per-slot indexing (round 4): a batch with a silent slot
+    (no decodes), a dense one (> 32 distinct decodes, so the rest launch fits some) and an ordinary
+    one decodes each slot exactly as that slot alone; the silent slot's residual is its samples."""
+    import ctypes
+    from ft8_demodulator_amd import _lib
+    from ft8_demodulator_amd._pipeline import SlotDecoder, make_params
+    xa, ta = _slots(gpu, 1, 70, seed=501, snr=(-12.0, 0.0))
+    xb, tb = _slots(gpu, 1, 20, seed=502)
+    silent = gpu.zeros_like(xa)
+    x = gpu.cat([xa, silent, xb]).contiguous()
+    kw = dict(sample_rate=12000, max_candidates=300, min_score=2, flags=_lib.FT8_FLAG_TOPK | _lib.FT8_FLAG_SUBTRACT)
+    dec = SlotDecoder(**kw)
+    batch = dec.records(x, _lib.FT8_F32)
+    assert len(batch[1]) == 0
+    n_dense = len(set(bytes(r["payload"]) for r in batch[0] if r["pass_index"] == 0))
+    assert n_dense > 32, n_dense
+    for s in (0, 2):
+        single = SlotDecoder(**kw).records(x[s:s + 1], _lib.FT8_F32)[0]
+        b = batch[s].copy()
+        b["slot"] = 0
+        assert np.array_equal(b.view(np.uint8), single.view(np.uint8)), s
+        assert set(bytes(r["payload"]) for r in batch[s]) <= (ta[0] if s == 0 else tb[0])
+    # the residual of the silent slot is its (zero) samples; the dense slot lost most of its energy
+    d1 = SlotDecoder(**dict(kw, flags=_lib.FT8_FLAG_TOPK))
+    out, counts = d1.run(x)
+    N = x.shape[1]
+    p = make_params(d1.plan(N), 300, 2, 20, _lib.FT8_FLAG_TOPK)
+    res = gpu.empty_like(x)
+    ctx = d1.ctx
+    ctx.check(_lib.lib().ft8_subtract(ctx.handle, _lib.ptr(x), _lib.FT8_F32, _lib.ptr(res), N, 3, N, ctypes.byref(p),
+                                      _lib.ptr(out), _lib.ptr(counts), d1.cap, _lib.stream_handle()), "ft8_subtract")
+    gpu.cuda.synchronize()
+    assert float(res[1].abs().max()) == 0.0
+    assert float((res[0].double() ** 2).sum()) < float((x[0].double() ** 2).sum())
+
+
 def test_make_slots_gpu_matches_cpu(gpu):
     """The benchmark generator on the GPU (HIP transmit chain) equals the PyTorch CPU restatement."""
     from ft8_demodulator_amd import synth
