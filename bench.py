@@ -641,6 +641,10 @@ def drift_correct(dev, n_sig=256, reps=5):
     # de-rotation: stage 1 reads 16 B and writes 16 B per sample, stage 2 reads and writes 16 B
     rot_bytes = n_sig * n * 64
     rot_ms = tm["drift_derotate"][0] / reps
+    # the complex128 STFT-argmax decides frames in float32 where its error bound settles them and
+    # redoes the rest in float64 (stft.hip, launch_c3840_screened): the last call's split
+    n_re, n_fr = ctypes.c_int64(0), ctypes.c_int64(0)
+    ctx.check(_lib.lib().ft8_stft_screen_stats(ctx.handle, ctypes.byref(n_re), ctypes.byref(n_fr)), "ft8_stft_screen_stats")
     del x, out
     return {"workload": f"correct_frequency_drift on {n_sig} complex128 beacons x {n} samples (12 kHz, "
                         "signal between two zero-signal pads as in test_correction.py), drift U(50,150) Hz/s, "
@@ -648,7 +652,10 @@ def drift_correct(dev, n_sig=256, reps=5):
             "signals_per_s": n_sig * reps / dt, "ms_per_launch": dt / reps * 1e3,
             "full_fits": int(ok.sum()), "median_abs_rate_err_hz_per_s": float(np.median(np.abs(est[ok] - true[ok]))),
             "stages_ms": stages,
-            "roofline": {"kernel": "k_stft (argmax epilogue, complex128)", "bound": "fp64-valu", "achieved": tf,
+            "stft_screen": {"frames": int(n_fr.value), "redone_f64": int(n_re.value),
+                            "what": "the last STFT-argmax call's frames, and those the float32 pass left to float64"},
+            "roofline": {"kernel": "k_stftc3840 (argmax epilogue, complex128: float32 screening + float64 redo)",
+                         "bound": "fp64-valu", "achieved": tf,
                          "peak": FP64_VECTOR_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": tf / FP64_VECTOR_PEAK_TFLOPS,
                          "flops_per_launch": fft_flops, "launch_ms": stft_ms},
             "roofline_derotate": {"kernel": "k_derotate1 + k_derotate2", "bound": "hbm",

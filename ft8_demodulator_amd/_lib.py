@@ -138,6 +138,7 @@ def lib():
             "ft8_pack_bytes": ([i32, i32], i64),
             "ft8_subtract_fits": ([vp, vp, i32, i32, vp], ctypes.c_int),
             "ft8_stft_method": ([vp, i32, i32, i32, i64, ctypes.c_int], ctypes.c_int),
+            "ft8_stft_screen_stats": ([vp, ctypes.POINTER(i64), ctypes.POINTER(i64)], ctypes.c_int),
             "ft8_pack_decodes": ([vp, vp, vp, i32, i32, i32, i32, vp, vp, vp], ctypes.c_int),
         }
         for name, (args, res) in sig.items():
@@ -182,7 +183,7 @@ EXPORTED_SYMBOLS = (
     "ft8_crc14", "ft8_ldpc_check", "ft8_set_timing", "ft8_get_timing", "ft8_get_counters", "ft8_set_pipeline",
     "ft8_encode", "ft8_synthesize", "ft8_subtract", "ft8_stft_argmax", "ft8_drift_fit", "ft8_drift_correct",
     "ft8_build_id", "ft8_build_flags", "ft8_replay_stage", "ft8_set_timing_stages", "ft8_sync_score",
-    "ft8_pack_bytes", "ft8_pack_decodes", "ft8_subtract_fits", "ft8_stft_method")
+    "ft8_pack_bytes", "ft8_pack_decodes", "ft8_subtract_fits", "ft8_stft_method", "ft8_stft_screen_stats")
 
 
 def limits():

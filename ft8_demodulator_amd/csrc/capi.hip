@@ -64,6 +64,7 @@ struct ft8_ctx {
   // FT8_FLAG_SUBTRACT: residual samples, per-record fits, pass-1 / pass-2 records
   DevBuf residual, sub_est, sub_list, out1, counts1, out2, counts2;
   DevBuf screen;  // complex128 argmax STFT: [count][frames] uncertain-frame list (stft.hip)
+  int64_t screen_frames = 0;  // frames of the last screened call (0: the last call was not screened)
   int sub_slots = 0, sub_cap = 0;  // shape of the fits in sub_est (ft8_subtract_fits)
   // cumulative GFSK pulse of the transmit chain for one nsps (double and float)
   int gfsk_nsps = 0;
@@ -868,6 +869,9 @@ int stft_argmax_core(ft8_ctx* c, const void* x, int dtype, int64_t n_samples, in
     if ((rc = ensure(c, c->screen, sizeof(int32_t) * (frames + 1)))) return rc;
     L.screen_count = (int32_t*)c->screen.p;
     L.screen_list = L.screen_count + 1;
+    c->screen_frames = (int64_t)frames;
+  } else {
+    c->screen_frames = 0;
   }
   StageTimer tm(c, 8, s);
   hipError_t e = launch_stft(L, s);
@@ -1034,6 +1038,20 @@ int ft8_stft(ft8_ctx* c, const void* d_samples, int dtype, int64_t n_samples, in
   if (!c || !p || (!d_samples && n_slots > 0) || (!d_wf && n_slots > 0)) return fail(c, FT8_E_ARG, "null argument");
   DeviceGuard dg(c->device);
   return do_stft(c, d_samples, dtype, n_samples, n_slots, slot_stride, p, d_wf, (hipStream_t)stream);
+}
+
+int ft8_stft_screen_stats(ft8_ctx* c, int64_t* frames_redone, int64_t* frames) {
+  if (!c || !frames_redone || !frames) return fail(c, FT8_E_ARG, "null argument");
+  *frames_redone = 0;
+  *frames = c->screen_frames;
+  if (c->screen_frames == 0) return FT8_OK;
+  DeviceGuard dg(c->device);
+  int32_t n = 0;
+  hipError_t e = hipDeviceSynchronize();
+  if (e == hipSuccess) e = hipMemcpy(&n, c->screen.p, sizeof(int32_t), hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return hipfail(c, e, "screen count");
+  *frames_redone = n;
+  return FT8_OK;
 }
 
 int ft8_stft_method(ft8_ctx* c, int32_t fs, int32_t bpt, int32_t sps, int64_t n, int dtype) {

@@ -142,6 +142,11 @@ int ft8_stft(ft8_ctx* ctx, const void* d_samples, int dtype, int64_t n_samples, 
 #define FT8_STFT_DFT 3
 int ft8_stft_method(ft8_ctx* ctx, int32_t sample_rate, int32_t bins_per_tone, int32_t steps_per_symbol,
                     int64_t n_samples, int dtype);
+/* Introspection of the last ft8_stft_argmax / drift STFT on complex128 input at the 3840-point
+ * geometry, which decides each frame's argmax in float32 where a rounding-error bound settles it
+ * and redoes the others in float64: *frames_redone = the float64 frames of that call, *frames =
+ * all its frames (0 / 0 when the last call took another path).  Synchronises the device. */
+int ft8_stft_screen_stats(ft8_ctx* ctx, int64_t* frames_redone, int64_t* frames);
 
 /* ---- stage 2: Costas sync score grid + candidate selection ---------------------------------
  * Replaces ft8_sync_score / ft8_find_candidates (ft8_decode.py:47-149).  d_wf as produced by
