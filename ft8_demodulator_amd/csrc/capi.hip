@@ -864,7 +864,9 @@ int stft_argmax_core(ft8_ctx* c, const void* x, int dtype, int64_t n_samples, in
   L.window = w->w;
   L.scale = w->scale;
   L.argmax = idx;
-  if (dtype == FT8_C128 && !L.plan.dft && !L.plan.blue && g.nfft == 3840 && g.nperseg == 1920) {
+  // the geometries launch_stft sends to k_stftc3840 (stft.hip)
+  if (dtype == FT8_C128 && !L.plan.dft && !L.plan.blue && g.nfft == 3840 && g.nperseg == 1920 &&
+      (g.hop == 240 || g.hop == 480 || g.hop == 960 || g.hop == 1920)) {
     const size_t frames = (size_t)n_slots * (size_t)(p->t_hi - p->t_lo);
     if ((rc = ensure(c, c->screen, sizeof(int32_t) * (frames + 1)))) return rc;
     L.screen_count = (int32_t*)c->screen.p;

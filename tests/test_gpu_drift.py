@@ -52,6 +52,47 @@ def test_stft_argmax_equals_argmax_of_waterfall(gpu):
         assert np.array_equal(idx.cpu().numpy(), np.argmax(wf.cpu().numpy(), axis=2)), (dtype, fs, sps)
 
 
+def test_screened_complex128_argmax_equals_float64(gpu):
+    """complex128 STFT-argmax at the 3840-point geometry decides frames in float32 where its error
+    bound settles them and redoes the rest in float64 (round 4): the result equals np.argmax of the
+    float64 dB rows on frames built to defeat the screen -- all-zero stretches (every level equal),
+    tones exactly between two bins and a pair of equal-power tones (near-equal top levels), a tone
+    far below the 1e-12 floor, huge amplitudes -- and plain noise; the split is reported."""
+    from ft8_demodulator_amd import _lib
+    import ctypes
+    fs, sps, n = 12000, 8, 1920 * 40
+    nperseg, hop, nfft, T = _lib.geometry(fs, 2, sps, n)
+    F = (nfft + 1) // 2
+    rng = np.random.default_rng(77)
+    tt = np.arange(n) / fs
+    x = np.zeros((5, n), np.complex128)
+    x[0] = rng.normal(size=n) + 1j * rng.normal(size=n)                     # noise
+    x[1, n // 3:] = np.exp(2j * np.pi * (1000.0 + 6.25 / 2 * 0.5) * tt[n // 3:])  # between bins, then silence before
+    x[2] = np.exp(2j * np.pi * 500.0 * tt) + np.exp(2j * np.pi * 1500.0 * tt)   # two equal tones
+    x[2] += 1e-3 * (rng.normal(size=n) + 1j * rng.normal(size=n))
+    x[3] = 1e-9 * np.exp(2j * np.pi * 800.0 * tt)                               # below the level floor
+    x[4] = 1e150 * (rng.normal(size=n) + 1j * rng.normal(size=n))               # float32 overflows
+    ctx = _lib.context()
+    t = gpu.from_numpy(x).cuda()
+    p = _lib.Ft8Params(sample_rate=fs, bins_per_tone=2, steps_per_symbol=sps, f_lo=0, f_hi=F, t_lo=0, t_hi=T)
+    wf = gpu.empty((5, T, F), dtype=gpu.float64, device="cuda")
+    idx = gpu.empty((5, T), dtype=gpu.int32, device="cuda")
+    s = gpu.cuda.current_stream().cuda_stream
+    ctx.check(_lib.lib().ft8_stft(ctx.handle, t.data_ptr(), _lib.FT8_C128, n, 5, n, ctypes.byref(p), wf.data_ptr(), s),
+              "stft")
+    ctx.check(_lib.lib().ft8_stft_argmax(ctx.handle, t.data_ptr(), _lib.FT8_C128, n, 5, n, ctypes.byref(p),
+                                         idx.data_ptr(), s), "argmax")
+    got, want = idx.cpu().numpy(), np.argmax(wf.cpu().numpy(), axis=2)
+    assert np.array_equal(got, want), [np.flatnonzero(got[k] != want[k])[:5] for k in range(5)]
+    redone, frames = ctypes.c_int64(), ctypes.c_int64()
+    ctx.check(_lib.lib().ft8_stft_screen_stats(ctx.handle, ctypes.byref(redone), ctypes.byref(frames)), "stats")
+    assert frames.value == 5 * T
+    # the silent frames (every level 1e-12) and the slot float32 cannot hold go to float64; most do not
+    silent = (n // 3 - nperseg) // hop + 1
+    assert redone.value >= T + silent, (redone.value, T, silent)
+    assert redone.value < 3 * T
+
+
 def test_argmax_matches_reference_goldens(gpu, drift_golden, drift_inputs):
     from ft8_demodulator_amd import _lib
     import ctypes

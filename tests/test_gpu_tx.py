@@ -298,7 +298,23 @@ def test_subtract_mixed_batch_with_silent_and_dense_slots(gpu):
     import ctypes
     from ft8_demodulator_amd import _lib
     from ft8_demodulator_amd._pipeline import SlotDecoder, make_params
-    xa, ta = _slots(gpu, 1, 70, seed=501, snr=(-12.0, 0.0))
+    from ft8_demodulator_amd import ft8_generator as G
+    # the dense slot: 42 strong signals on a 62.5 Hz grid (no two share a channel), staggered starts
+    rng = np.random.default_rng(501)
+    fs, N, n_sig = 12000, 180000, 42
+    pays = rng.integers(0, 256, size=(n_sig, 10), dtype=np.uint8)
+    pays[:, 9] &= 0xF8
+    _, _, tones = G.encode_batch(pays)
+    sig = np.zeros(n_sig, dtype=_lib.TX_SIGNAL_DTYPE)
+    sig["f0"] = 200.0 + 62.5 * np.arange(n_sig)
+    sig["amplitude"] = np.sqrt(2 * 10 ** (rng.uniform(-5.0, 5.0, n_sig) / 10))
+    sig["phase"] = rng.uniform(0, 2 * np.pi, n_sig)
+    sig["start"] = (rng.uniform(0.2, 1.5, n_sig) * fs).astype(np.int64)
+    g_ = gpu.Generator(device="cuda")
+    g_.manual_seed(501)
+    xa = gpu.randn((1, N), generator=g_, device="cuda", dtype=gpu.float32)
+    G.synthesize(tones, sig, 1, N, fs, out=xa)
+    ta = [set(bytes(p_) for p_ in pays)]
     xb, tb = _slots(gpu, 1, 20, seed=502)
     silent = gpu.zeros_like(xa)
     x = gpu.cat([xa, silent, xb]).contiguous()
