@@ -73,24 +73,30 @@ def test_screened_complex128_argmax_equals_float64(gpu):
     x[3] = 1e-9 * np.exp(2j * np.pi * 800.0 * tt)                               # below the level floor
     x[4] = 1e150 * (rng.normal(size=n) + 1j * rng.normal(size=n))               # float32 overflows
     ctx = _lib.context()
-    t = gpu.from_numpy(x).cuda()
     p = _lib.Ft8Params(sample_rate=fs, bins_per_tone=2, steps_per_symbol=sps, f_lo=0, f_hi=F, t_lo=0, t_hi=T)
-    wf = gpu.empty((5, T, F), dtype=gpu.float64, device="cuda")
-    idx = gpu.empty((5, T), dtype=gpu.int32, device="cuda")
     s = gpu.cuda.current_stream().cuda_stream
-    ctx.check(_lib.lib().ft8_stft(ctx.handle, t.data_ptr(), _lib.FT8_C128, n, 5, n, ctypes.byref(p), wf.data_ptr(), s),
-              "stft")
-    ctx.check(_lib.lib().ft8_stft_argmax(ctx.handle, t.data_ptr(), _lib.FT8_C128, n, 5, n, ctypes.byref(p),
-                                         idx.data_ptr(), s), "argmax")
-    got, want = idx.cpu().numpy(), np.argmax(wf.cpu().numpy(), axis=2)
-    assert np.array_equal(got, want), [np.flatnonzero(got[k] != want[k])[:5] for k in range(5)]
-    redone, frames = ctypes.c_int64(), ctypes.c_int64()
-    ctx.check(_lib.lib().ft8_stft_screen_stats(ctx.handle, ctypes.byref(redone), ctypes.byref(frames)), "stats")
-    assert frames.value == 5 * T
-    # the silent frames (every level 1e-12) and the slot float32 cannot hold go to float64; most do not
+    redone = []
+    # one slot per call, so the split is known per kind of input
+    for k in range(5):
+        t = gpu.from_numpy(x[k:k + 1].copy()).cuda()
+        wf = gpu.empty((1, T, F), dtype=gpu.float64, device="cuda")
+        idx = gpu.empty((1, T), dtype=gpu.int32, device="cuda")
+        ctx.check(_lib.lib().ft8_stft(ctx.handle, t.data_ptr(), _lib.FT8_C128, n, 1, n, ctypes.byref(p), wf.data_ptr(), s),
+                  "stft")
+        ctx.check(_lib.lib().ft8_stft_argmax(ctx.handle, t.data_ptr(), _lib.FT8_C128, n, 1, n, ctypes.byref(p),
+                                             idx.data_ptr(), s), "argmax")
+        got, want = idx.cpu().numpy()[0], np.argmax(wf.cpu().numpy()[0], axis=1)
+        assert np.array_equal(got, want), (k, np.flatnonzero(got != want)[:5])
+        r, fr = ctypes.c_int64(), ctypes.c_int64()
+        ctx.check(_lib.lib().ft8_stft_screen_stats(ctx.handle, ctypes.byref(r), ctypes.byref(fr)), "stats")
+        assert fr.value == T
+        redone.append(r.value)
+    print("frames redone in float64 per slot (of %d):" % T, redone)
     silent = (n // 3 - nperseg) // hop + 1
-    assert redone.value >= T + silent, (redone.value, T, silent)
-    assert redone.value < 3 * T
+    assert redone[0] <= T // 20                 # noise: float32 settles almost every frame
+    assert redone[1] >= silent                  # all-zero frames: every level equal
+    assert redone[4] == T                       # float32 overflows
+    assert redone[2] < T                        # equal tones: the noise separates most frames
 
 
 def test_argmax_matches_reference_goldens(gpu, drift_golden, drift_inputs):
