@@ -871,6 +871,14 @@ int stft_argmax_core(ft8_ctx* c, const void* x, int dtype, int64_t n_samples, in
     if ((rc = ensure(c, c->screen, sizeof(int32_t) * (frames + 1)))) return rc;
     L.screen_count = (int32_t*)c->screen.p;
     L.screen_list = L.screen_count + 1;
+    // the screening pass transforms in float32: its own twiddles and window
+    FftPlan fp;
+    if ((rc = get_plan(c, g.nfft, true, false, g.nperseg, &fp))) return rc;
+    WinEntry* wf32 = nullptr;
+    if ((rc = get_window(c, g.nperseg, false, &wf32))) return rc;
+    if (fp.P != 3840 || fp.dft || fp.blue) return fail(c, FT8_E_UNSUPPORTED, "float32 screening plan");
+    L.screen_tw = fp.tw;
+    L.screen_window = wf32->w;
     c->screen_frames = (int64_t)frames;
   } else {
     c->screen_frames = 0;

@@ -95,6 +95,8 @@ struct StftLaunch {
                            // (a direct-DFT plan then writes the dB rows to `out` first)
   int32_t* screen_list;    // non-null (complex128 argmax, 3840-point geometry): float32 screening
   int32_t* screen_count;   // with the uncertain frames listed here and redone in float64
+  const void* screen_tw;     // the screening pass's float32 twiddles (W_3840^m) and window
+  const void* screen_window;
   FftPlan plan;
 };
 hipError_t launch_stft(const StftLaunch& a, hipStream_t s);

@@ -809,31 +809,35 @@ hipError_t launch_c3840_screened(const StftLaunch& L, StftArgs a, hipStream_t s)
   a.per_xcd = (int)(((int64_t)chunks * L.n_slots + 7) / 8);
   const size_t lds32 = (size_t)(kC38P + kC38P / 16 + 1) * sizeof(cplx<float>) + 16 * sizeof(float) + 1920 * sizeof(float);
   const size_t lds64 = (size_t)(kC38P + kC38P / 16 + 1) * sizeof(cplx<double>) + 16 * sizeof(double) + 1920 * sizeof(double);
-  auto go = [&](auto kern, dim3 grid, size_t lds) {
+  auto go = [&](auto kern, dim3 grid, size_t lds, const StftArgs& args) {
     if (lds > 64 * 1024) {
       hipError_t e2 = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                           (int)lds);
       if (e2 != hipSuccess) return e2;
     }
-    hipLaunchKernelGGL(kern, grid, dim3(kC38Threads), lds, s, a);
+    hipLaunchKernelGGL(kern, grid, dim3(kC38Threads), lds, s, args);
     return hipGetLastError();
   };
   const dim3 g1((unsigned)(8 * a.per_xcd));
   const int64_t frames = (int64_t)a.nt_out * L.n_slots;
+  // the screen transforms in float32 (the plan's tables are float64 for complex128 input)
+  StftArgs a32 = a;
+  a32.tw = L.screen_tw;
+  a32.window = L.screen_window;
   const dim3 g2((unsigned)std::min<int64_t>(frames, 512));  // two float64 workgroups per CU
   switch (L.hop) {
     case 240:
-      if ((e = go(k_stftc3840<double, float, 1, 2>, g1, lds32)) != hipSuccess) return e;
-      return go(k_stftc3840<double, double, 1, 3>, g2, lds64);
+      if ((e = go(k_stftc3840<double, float, 1, 2>, g1, lds32, a32)) != hipSuccess) return e;
+      return go(k_stftc3840<double, double, 1, 3>, g2, lds64, a);
     case 480:
-      if ((e = go(k_stftc3840<double, float, 2, 2>, g1, lds32)) != hipSuccess) return e;
-      return go(k_stftc3840<double, double, 2, 3>, g2, lds64);
+      if ((e = go(k_stftc3840<double, float, 2, 2>, g1, lds32, a32)) != hipSuccess) return e;
+      return go(k_stftc3840<double, double, 2, 3>, g2, lds64, a);
     case 960:
-      if ((e = go(k_stftc3840<double, float, 4, 2>, g1, lds32)) != hipSuccess) return e;
-      return go(k_stftc3840<double, double, 4, 3>, g2, lds64);
+      if ((e = go(k_stftc3840<double, float, 4, 2>, g1, lds32, a32)) != hipSuccess) return e;
+      return go(k_stftc3840<double, double, 4, 3>, g2, lds64, a);
     default:
-      if ((e = go(k_stftc3840<double, float, 8, 2>, g1, lds32)) != hipSuccess) return e;
-      return go(k_stftc3840<double, double, 8, 3>, g2, lds64);
+      if ((e = go(k_stftc3840<double, float, 8, 2>, g1, lds32, a32)) != hipSuccess) return e;
+      return go(k_stftc3840<double, double, 8, 3>, g2, lds64, a);
   }
 }
 
@@ -1148,7 +1152,8 @@ hipError_t launch_stft(const StftLaunch& L, hipStream_t s) {
   // complex input in the beacon receiver's geometry (12 kHz: nfft 3840, nperseg 1920, hop 240 M)
   if ((L.dtype == FT8_C64 || L.dtype == FT8_C128) && L.nfft == kC38P && L.nperseg == 1920 && a.P == kC38P &&
       (L.hop == 240 || L.hop == 480 || L.hop == 960 || L.hop == 1920)) {
-    if (L.dtype == FT8_C128 && L.argmax && L.screen_list) return launch_c3840_screened(L, a, s);
+    if (L.dtype == FT8_C128 && L.argmax && L.screen_list && L.screen_tw && L.screen_window)
+      return launch_c3840_screened(L, a, s);
     if (L.dtype == FT8_C128) return launch_c3840<double, double>(L, a, s);
     return launch_c3840<float, float>(L, a, s);
   }
