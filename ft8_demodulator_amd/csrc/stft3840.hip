@@ -233,7 +233,8 @@ __global__ __launch_bounds__(kThreads38, 4) void k_stft3840p(Args a) {
   __shared__ f2 buf[2][kBuf];  // frame A, frame B
   __shared__ f2 wl[kP / 2];    // the window as pairs (w[2n], w[2n+1]): 39.4 KB in all, four workgroups per CU
   const int t = threadIdx.x;
-  const int role = t >> 7;  // stages 1 and 3: the frame this thread works on (A = 0, B = 1)
+  // stages 1 and 3: the frame this thread works on (A = 0, B = 1); wave-uniform, so in an SGPR
+  const int role = __builtin_amdgcn_readfirstlane(t >> 7);
   const int u = t & 127;    // ... and its index there
   const int chunks = (a.nt_out + kChunk - 1) / kChunk;
   const int slot = blockIdx.x / chunks;
@@ -246,7 +247,7 @@ __global__ __launch_bounds__(kThreads38, 4) void k_stft3840p(Args a) {
   // wave, 32 lanes over (see the epilogue below): lanes 0..31 of the frame's first wave take u =
   // 0..31, lane 32 u = 64, lanes 33..63 u = 127..97; the second wave's lanes 0..31 u = 32..63 and
   // lanes 32..63 u = 96..65
-  const int lane = t & 63, half = (t >> 6) & 1;
+  const int lane = t & 63, half = __builtin_amdgcn_readfirstlane((t >> 6) & 1);
   const int u3 = !FULL ? u : half == 0 ? (lane < 32 ? lane : lane == 32 ? 64 : 160 - lane) : (lane < 32 ? 32 + lane : 128 - lane);
   f2 s2 = a.tw[15 * (t & 15)], s3 = a.tw[u3];
   const bool rec_post = a.f_lo + a.nf_out <= kP;
