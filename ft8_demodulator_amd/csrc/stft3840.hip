@@ -21,7 +21,10 @@
 // frames' radix-8 butterfly j = t on 240 threads, the epilogue both frames' bins; one LDS image per
 // frame with every stage in place, twiddles formed in registers by recurrence from per-thread
 // seeds; a workgroup walks a run of consecutive frames of one slot, each thread loading its next
-// frame's raw samples as soon as stage 1 has consumed the current ones.
+// frame's raw samples as soon as stage 1 has consumed the current ones.  With the full band kept
+// (the decoder's waterfall; round 4) the epilogue runs on stage 3's registers: stage 3's threads
+// are permuted so every bin pair (k, P - k) lies in one wave, 32 lanes apart, and the partner
+// values cross by ds_bpermute -- stage 3 writes nothing back, one barrier per pass less.
 #include "ft8_internal.h"
 
 namespace ft8 {
