@@ -21,7 +21,10 @@
 // frames' radix-8 butterfly j = t on 240 threads, the epilogue both frames' bins; one LDS image per
 // frame with every stage in place, twiddles formed in registers by recurrence from per-thread
 // seeds; a workgroup walks a run of consecutive frames of one slot, each thread loading its next
-// frame's raw samples as soon as stage 1 has consumed the current ones.
+// frame's raw samples as soon as stage 1 has consumed the current ones.  With the full band kept
+// (the decoder's waterfall; round 4) the epilogue runs on stage 3's registers: stage 3's threads
+// are permuted so every bin pair (k, P - k) lies in one wave, 32 lanes apart, and the partner
+// values cross by ds_bpermute -- stage 3 writes nothing back, one barrier per pass less.
 #include "ft8_internal.h"
 
 namespace ft8 {
@@ -226,13 +229,15 @@ typedef __attribute__((address_space(3))) f2 lds_f2;
 __device__ __forceinline__ f2 lds_ld(const f2* p) { return *(const volatile lds_f2*)p; }
 __device__ __forceinline__ void lds_st(f2* p, f2 v) { *(volatile lds_f2*)p = v; }
 
-template <typename InT>
-__global__ __launch_bounds__(kThreads38) void k_stft3840p(Args a) {
+// FULL: every f >= 0 bin kept (no band mask; the decoder's waterfall), its epilogue fused into stage 3
+template <typename InT, bool FULL>
+__global__ __launch_bounds__(kThreads38, 4) void k_stft3840p(Args a) {
   FT8_RACE_PROLOGUE();
   __shared__ f2 buf[2][kBuf];  // frame A, frame B
   __shared__ f2 wl[kP / 2];    // the window as pairs (w[2n], w[2n+1]): 39.4 KB in all, four workgroups per CU
   const int t = threadIdx.x;
-  const int role = t >> 7;  // stages 1 and 3: the frame this thread works on (A = 0, B = 1)
+  // stages 1 and 3: the frame this thread works on (A = 0, B = 1); wave-uniform, so in an SGPR
+  const int role = __builtin_amdgcn_readfirstlane(t >> 7);
   const int u = t & 127;    // ... and its index there
   const int chunks = (a.nt_out + kChunk - 1) / kChunk;
   const int slot = blockIdx.x / chunks;
@@ -241,13 +246,21 @@ __global__ __launch_bounds__(kThreads38) void k_stft3840p(Args a) {
   // twiddle seeds: stage 2 W_128^k (k = t % 16), stage 3 W_1920^u, epilogue W_3840^(f_lo + t) and
   // its 256-bin step; their powers are formed by complex recurrence each pass (relative error
   // ~15 ulp, far inside the dB tolerance)
-  f2 s2 = a.tw[15 * (t & 15)], s3 = a.tw[u];
+  // stage 3's index: u, or (FULL) a permutation of u that puts bin k's partner P - k in the same
+  // wave, 32 lanes over (see the epilogue below): lanes 0..31 of the frame's first wave take u =
+  // 0..31, lane 32 u = 64, lanes 33..63 u = 127..97; the second wave's lanes 0..31 u = 32..63 and
+  // lanes 32..63 u = 96..65
+  const int lane = t & 63, half = __builtin_amdgcn_readfirstlane((t >> 6) & 1);
+  const int u3 = !FULL ? u : half == 0 ? (lane < 32 ? lane : lane == 32 ? 64 : 160 - lane) : (lane < 32 ? 32 + lane : 128 - lane);
+  f2 s2 = a.tw[15 * (t & 15)], s3 = a.tw[u3];
   const bool rec_post = a.f_lo + a.nf_out <= kP;
-  const bool full = a.f_lo == 0 && a.nf_out == kP;  // every f >= 0 bin kept (no band mask)
+  constexpr bool full = FULL;
   // 10 log10(v) = (10 log10 2) log2(v): v_log_f32 on a normal argument (v >= 1e-12)
   constexpr float kDb = 3.0102999566398119521f;
-  f2 p0 = a.post[min(a.f_lo + t, kP)];
-  const f2 pstep = a.post[kThreads38];
+  // post-twiddle seeds: the full band walks k = u + 128 r (stage 3's own bins), a band k = f_lo + t
+  // + 256 i
+  f2 p0 = full ? a.post[u3] : a.post[min(a.f_lo + t, kP)];
+  const f2 pstep = a.post[full ? 128 : kThreads38];
   const f2 qscale = splat(0.25f * a.scale);  // |2 X|^2 / 4 / (sum w)^2 (powers of two: exact)
 
   for (int n = t; n < kP / 2; n += kThreads38) wl[n] = *reinterpret_cast<const f2*>(a.window + 2 * n);
@@ -315,14 +328,14 @@ __global__ __launch_bounds__(kThreads38) void k_stft3840p(Args a) {
       }
     }
     __syncthreads();
-    // stage 3: radix 15, Ns = 128: j = u, natural order, in place (a thread writes the 15 positions
+    // stage 3: radix 15, Ns = 128: j = u3, natural order, in place (a thread writes the 15 positions
     // it read)
     if (mine) {
       f2 v[15], y[15];
 #pragma unroll
-      for (int r = 0; r < 15; ++r) v[r] = lds_ld(&img[pidx(u) + 136 * r]);  // pidx(u + 128 r)
-      if (u != 0) {
-        f2 w = s3;  // W_1920^(r u)
+      for (int r = 0; r < 15; ++r) v[r] = lds_ld(&img[pidx(u3) + 136 * r]);  // pidx(u3 + 128 r)
+      if (u3 != 0) {
+        f2 w = s3;  // W_1920^(r u3)
 #pragma unroll
         for (int r = 1; r < 15; ++r) {
           v[r] = cmul(v[r], w);
@@ -330,36 +343,62 @@ __global__ __launch_bounds__(kThreads38) void k_stft3840p(Args a) {
         }
       }
       dft15(v, y);
+      if constexpr (!FULL) {
 #pragma unroll
-      for (int r = 0; r < 15; ++r) lds_st(&img[pidx(u) + 136 * r], y[r]);
+        for (int r = 0; r < 15; ++r) lds_st(&img[pidx(u3) + 136 * r], y[r]);
+      } else {
+        // the epilogue from stage 3's registers (round 4).  The thread holds Z[u3 + 128 r]; bin k's
+        // partner P - k = (128 - u3) + 128 (14 - r) is element 14 - r of u = 128 - u3, 32 lanes
+        // over in this wave (u3 = 0 and 64: the thread itself, at 15 - r and 14 - r).  The thread
+        // takes the pairs of its r = 0..7 (r = 7 only for u3 <= 64: past it k > P / 2), so it needs
+        // its partner's 7..14: eight ds_bpermute pairs instead of the image written back and read
+        // again (the LDS store path was the kernel's busiest), and one barrier less per pass.
+        const bool self = half == 0 && (lane & 31) == 0;
+        const int src = (self ? lane : lane ^ 32) << 2;
+        if (half == 0) {
+          // u3 = 0 pairs r with its own 15 - r (r >= 1) and bin 0 with itself, where u3 = 64 pairs
+          // r with 14 - r: lane 0 offers itself its 8..14 and Z[0] in the slots of 7..14 (a
+          // wave-uniform branch, first waves only); its own y[7] (A of the pair (7, 8)) is kept
+          const bool z0 = lane == 0;
+          v[7] = y[7];
+#pragma unroll
+          for (int r = 7; r < 14; ++r) y[r] = z0 ? y[r + 1] : y[r];
+          y[14] = z0 ? y[0] : y[14];
+        } else {
+          v[7] = y[7];
+        }
+        f2 pr[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          pr[j].x = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(y[7 + j].x)));
+          pr[j].y = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(y[7 + j].y)));
+        }
+        f2 pw_k = p0;  // W_3840^k, k = u3 + 128 r
+        float* out = a.out + ((int64_t)slot * a.nt_out + f + role) * a.nf_out;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const f2 wk = pw_k;
+          if (r < 7) pw_k = cmul(pw_k, pstep);
+          if (r == 7 && u3 > 64) break;
+          const f2 A = r == 7 ? v[7] : y[r];
+          const f2 B = pr[7 - r];  // partner element 14 - r
+          const f2 sm = add_cj(A, B), df = sub_cj(A, B);
+          const f2 wd = cmul(wk, df);
+          const f2 re = re_pm(sm, wd), im = im_mp(sm, wd);  // (X1.x, X2.x), (X1.y, -X2.y)
+          const f2 pp = (re * re + im * im) * qscale + splat(1e-12f);
+          const f2 d = f2{__builtin_amdgcn_logf(pp.x), __builtin_amdgcn_logf(pp.y)} * splat(kDb);
+          const int k = u3 + 128 * r;
+          out[k] = d.x;
+          if (k != 0 && k != kP / 2) out[kP - k] = d.y;
+        }
+      }
     }
+    if constexpr (FULL) continue;  // the next pass's first barrier orders stage 3's reads before stage 1
     __syncthreads();
     // epilogue: real-signal spectrum X[k] = (s - i W_N^k d) / 2 with s = Z[k] + conj Z[P-k],
     // d = Z[k] - conj Z[P-k]; power, dB, kept bins -- frame A then frame B per bin block
     const int nfr = haveB ? 2 : 1;
-    if (full) {
-      // k and P - k share s and d: since W_N^(P-k) = -conj(W_N^k), 2 X[P-k] = conj(s + i W d)... the
-      // two spectra are (s.x + wd.y, s.y - wd.x) and (s.x - wd.y, -(s.y + wd.x)) for wd = W_N^k d;
-      // their real parts and imaginary parts are formed side by side, so both powers come from one
-      // packed multiply-add
-      f2 pw_k = p0;  // W_3840^k, k = t + 256 i
-      for (int k = t; k <= kP / 2; k += kThreads38) {
-        const f2 wk = pw_k;
-        pw_k = cmul(pw_k, pstep);
-        for (int q = 0; q < nfr; ++q) {
-          const f2 A = lds_ld(&buf[q][pidx(k)]);
-          const f2 B = lds_ld(&buf[q][pidx(k == 0 ? 0 : kP - k)]);
-          const f2 sm = add_cj(A, B), df = sub_cj(A, B);
-          const f2 wd = cmul(wk, df);
-          const f2 re = re_pm(sm, wd), im = im_mp(sm, wd);   // (X1.x, X2.x), (X1.y, -X2.y)
-          const f2 p = (re * re + im * im) * qscale + splat(1e-12f);
-          const float d1 = kDb * __builtin_amdgcn_logf(p.x), d2 = kDb * __builtin_amdgcn_logf(p.y);
-          float* out = a.out + ((int64_t)slot * a.nt_out + f + q) * a.nf_out;
-          out[k] = d1;
-          if (k != 0 && k != kP / 2) out[kP - k] = d2;
-        }
-      }
-    } else {
+    {
       f2 pw_k = p0;  // W_3840^k for k = f_lo + i (recurrence over i += 256)
       for (int i = t; i < a.nf_out; i += kThreads38) {
         const int k = a.f_lo + i;
@@ -404,8 +443,14 @@ hipError_t launch_stft3840(const StftLaunch& L, hipStream_t s) {
   if (a.nt_out <= 0 || a.nf_out <= 0 || L.n_slots <= 0) return hipSuccess;
   const int chunks = (a.nt_out + kChunk - 1) / kChunk;
   const dim3 grid((unsigned)(chunks * L.n_slots));
-  if (L.dtype == FT8_F32) hipLaunchKernelGGL(k_stft3840p<float>, grid, dim3(kThreads38), 0, s, a);
-  else hipLaunchKernelGGL(k_stft3840p<int16_t>, grid, dim3(kThreads38), 0, s, a);
+  const bool full = a.f_lo == 0 && a.nf_out == kP;
+  if (L.dtype == FT8_F32) {
+    if (full) hipLaunchKernelGGL((k_stft3840p<float, true>), grid, dim3(kThreads38), 0, s, a);
+    else hipLaunchKernelGGL((k_stft3840p<float, false>), grid, dim3(kThreads38), 0, s, a);
+  } else {
+    if (full) hipLaunchKernelGGL((k_stft3840p<int16_t, true>), grid, dim3(kThreads38), 0, s, a);
+    else hipLaunchKernelGGL((k_stft3840p<int16_t, false>), grid, dim3(kThreads38), 0, s, a);
+  }
   return hipGetLastError();
 }
 

@@ -49,14 +49,14 @@ __device__ __forceinline__ float ld_sample<int16_t>(const int16_t* x, int64_t i)
   return (float)x[i] / 32767.0f;  // read_wave_file scaling, as the STFT applies it
 }
 
-// change of G over the first i samples of symbol k (protocol timing: u = (k + 1) nsps + i),
-// relative to the symbol start; float is plenty inside one symbol
-__device__ __forceinline__ float dG(const int* E, const float* Pf, int nsps, int k, int i) {
-  return (float)E[k] * (Pf[i + 2 * nsps] - Pf[2 * nsps]) + (float)E[k + 1] * (Pf[i + nsps] - Pf[nsps]) +
-         (float)E[k + 2] * (Pf[i] - Pf[0]);
-}
-
 __device__ __forceinline__ float ramp_f(int n, int L, int nsps) { return tx::gfsk_ramp<float>(n, L, nsps, 0); }
+// the amplitude ramp at sample n of symbol k: 1 except in the first and last symbols (the ramps are
+// nsps / 8 long).  The ramp's cos and division are a call there: inlined, the compiler evaluated
+// them for every sample of every symbol (~60 of the per-sample loop's ~120 VALU instructions)
+__device__ __noinline__ float ramp_edge(int n, int L, int nsps) { return ramp_f(n, L, nsps); }
+__device__ __forceinline__ float ramp_at(int k, int n, int L, int nsps) {
+  return (k == 0 || k == tx::kSymbols - 1) ? ramp_edge(n, L, nsps) : 1.0f;
+}
 
 // k_sub_list: one wave per slot lists the records worth a fit -- ok, and the first record of the
 // slot carrying its payload (a crowded top-k slot decodes ~40 records for ~21 distinct messages) --
@@ -100,7 +100,7 @@ __global__ __launch_bounds__(kSubThreads) void k_sub_est(SubLaunch a) {
   // dynamic LDS: the decimated baseband z (phases 2-3), then the float pulse table (phase 4)
   extern __shared__ float4 s_dyn[];
   float2* s_z = reinterpret_cast<float2*>(s_dyn);
-  float* s_Pf = reinterpret_cast<float*>(s_dyn);
+  float4* s_D = s_dyn;  // phase 4: the pulse table's symbol-relative differences (see k_sub_apply)
   __shared__ float s_metric[kMaxHyp];
   __shared__ float2 s_st[(2 * kMf + 1) * 8];
   __shared__ int s_E[tx::kExt];
@@ -303,7 +303,10 @@ __global__ __launch_bounds__(kSubThreads) void k_sub_est(SubLaunch a) {
     const double cyc = (f0 * (double)k * nsps + 6.25 * (G - G0)) / fs;
     s_ph0[k] = (float)(cyc - floor(cyc));
   }
-  for (int i = threadIdx.x; i <= 3 * nsps; i += kSubThreads) s_Pf[i] = a.Pf[i];
+  for (int i = threadIdx.x; i < nsps; i += kSubThreads) {
+    const float* P = a.Pf;
+    s_D[i] = make_float4(P[i + 2 * nsps] - P[2 * nsps], P[i + nsps] - P[nsps], P[i] - P[0], 0.0f);
+  }
   __syncthreads();
 
   // ---- 4. complex amplitude per symbol (one wave per symbol at a time; a lane's samples of the
@@ -317,6 +320,7 @@ __global__ __launch_bounds__(kSubThreads) void k_sub_est(SubLaunch a) {
       const float ph = s_ph0[k];
       const int64_t nsym = start + (int64_t)k * nsps;
       const bool inside = nsym >= 0 && nsym + nsps <= a.n_samples;
+      const float E0 = (float)s_E[k], E1 = (float)s_E[k + 1], E2 = (float)s_E[k + 2];
       for (int i0 = lane; i0 < nsps; i0 += kPf * kWave) {
         float v[kPf];
         const InT* xp = x + nsym + i0;
@@ -333,7 +337,8 @@ __global__ __launch_bounds__(kSubThreads) void k_sub_est(SubLaunch a) {
           const int64_t n = nsym + i;
           if (i >= nsps || !(inside || (n >= 0 && n < a.n_samples))) continue;
           const float rp = ramp_f(k * nsps + i, L, nsps);
-          const float cyc = ph + (float)i * f0r + sr * dG(s_E, s_Pf, nsps, k, i);
+          const float4 dd = s_D[i];  // the change of G over the symbol's first i samples
+          const float cyc = ph + (float)i * f0r + sr * (E0 * dd.x + E1 * dd.y + E2 * dd.z);
           const float fr = __builtin_amdgcn_fractf(cyc);  // v_sin / v_cos take revolutions
           const float sn = __builtin_amdgcn_sinf(fr), cs = __builtin_amdgcn_cosf(fr);
           const float vr = v[u] * rp;
@@ -378,7 +383,7 @@ __global__ __launch_bounds__(kSubThreads) void k_sub_est(SubLaunch a) {
 
 constexpr int kApPer = 16;
 constexpr int kApTile = kSubThreads * kApPer;
-constexpr int kApFits = 8;                     // fits staged in LDS per batch
+constexpr int kApFits = 4;                     // fits staged in LDS per batch
 constexpr int kApList = 1024;                  // overlapping fits listed per pass over the records
 
 // One workgroup per (slot, tile of 4096 samples).  Wave 0 lists the fits that overlap the tile, in
@@ -396,7 +401,11 @@ __global__ __launch_bounds__(kSubThreads) void k_sub_apply(SubLaunch a) {
   __shared__ float s_f0r[kApFits];
   __shared__ short s_list[kApList];
   __shared__ int s_nlist;
-  extern __shared__ float s_Pf[];  // float pulse table [3 nsps + 1]
+  // the pulse table's three symbol-relative differences per in-symbol offset i, one float4 each:
+  // (P[i + 2 nsps] - P[2 nsps], P[i + nsps] - P[nsps], P[i] - P[0]) -- one ds_read_b128 and no
+  // subtractions per sample instead of six reads and three subtractions (same values: the
+  // subtractions of the pulse table the phase is built from)
+  extern __shared__ float4 s_D[];
   const int slot = blockIdx.y;
   const int64_t t0 = (int64_t)blockIdx.x * kApTile;
   const int nsps = a.nsps, L = tx::kSymbols * nsps;
@@ -406,7 +415,10 @@ __global__ __launch_bounds__(kSubThreads) void k_sub_apply(SubLaunch a) {
   float acc[kApPer];
 #pragma unroll
   for (int k = 0; k < kApPer; ++k) acc[k] = 0.f;
-  for (int i = threadIdx.x; i <= 3 * nsps; i += kSubThreads) s_Pf[i] = a.Pf[i];
+  for (int i = threadIdx.x; i < nsps; i += kSubThreads) {
+    const float* P = a.Pf;
+    s_D[i] = make_float4(P[i + 2 * nsps] - P[2 * nsps], P[i + nsps] - P[nsps], P[i] - P[0], 0.0f);
+  }
   for (int j0 = 0; j0 < cnt; j0 += kApList) {
     __syncthreads();  // the previous list is consumed
     if (threadIdx.x < kWave) {
@@ -463,9 +475,9 @@ __global__ __launch_bounds__(kSubThreads) void k_sub_apply(SubLaunch a) {
         for (int kk = 0; kk < kApPer; ++kk) {
           const int64_t nabs = t0 + threadIdx.x + (int64_t)kk * kSubThreads;
           if (k >= 0 && k < tx::kSymbols && nabs < a.n_samples) {
-            // dG of tx_device.h's pulse table (the same float operations as dG())
-            const float g = E[k] * (s_Pf[i + 2 * nsps] - s_Pf[2 * nsps]) + E[k + 1] * (s_Pf[i + nsps] - s_Pf[nsps]) +
-                            E[k + 2] * (s_Pf[i] - s_Pf[0]);
+            // the change of G over the symbol's first i samples (tx_device.h's pulse table)
+            const float4 dd = s_D[i];
+            const float g = E[k] * dd.x + E[k + 1] * dd.y + E[k + 2] * dd.z;
             const float cyc = s_ph0[f][k] + (float)i * f0r + sr * g;
             const float fr = __builtin_amdgcn_fractf(cyc);  // v_sin / v_cos take revolutions
             const float sn = __builtin_amdgcn_sinf(fr), cs = __builtin_amdgcn_cosf(fr);
@@ -474,7 +486,7 @@ __global__ __launch_bounds__(kSubThreads) void k_sub_apply(SubLaunch a) {
             const float2 o = t < 0.f ? s_A[f][k > 0 ? k - 1 : 0] : s_A[f][k < tx::kSymbols - 1 ? k + 1 : k];
             const float2 A = t < 0.f ? make_float2(c.x + t * (c.x - o.x), c.y + t * (c.y - o.y))
                                      : make_float2(c.x + t * (o.x - c.x), c.y + t * (o.y - c.y));
-            acc[kk] += ramp_f(k * nsps + i, L, nsps) * (A.x * cs - A.y * sn);
+            acc[kk] += ramp_at(k, k * nsps + i, L, nsps) * (A.x * cs - A.y * sn);
           }
           i += kSubThreads;
           while (i >= nsps) {
@@ -545,7 +557,7 @@ hipError_t launch_sub_est(const SubLaunch& a, hipStream_t s) {
     // kSubRecStride fits
     const unsigned grid_rest = (unsigned)(((a.n_slots + 7) / 8) * 8 * (int64_t)kSubRestStride);
     const size_t mz = (size_t)tx::kSymbols * a.Q + 2 * (a.Q / (2 * (a.nsps / a.hop)) + 2);
-    const size_t lds = std::max(mz * sizeof(float2), (size_t)(3 * a.nsps + 1) * sizeof(float));
+    const size_t lds = std::max(mz * sizeof(float2), (size_t)a.nsps * sizeof(float4));
     if (a.dtype == FT8_I16) {
       hipLaunchKernelGGL((k_sub_est<int16_t, false>), dim3(grid), dim3(kSubThreads), lds, s, a);
       if (a.cap > kSubRecStride) hipLaunchKernelGGL((k_sub_est<int16_t, true>), dim3(grid_rest), dim3(kSubThreads), lds, s, a);
@@ -561,7 +573,7 @@ hipError_t launch_sub_est(const SubLaunch& a, hipStream_t s) {
 hipError_t launch_sub_apply(const SubLaunch& a, hipStream_t s) {
   if (a.n_slots <= 0 || a.n_samples <= 0) return hipSuccess;
   dim3 g2((unsigned)((a.n_samples + kApTile - 1) / kApTile), (unsigned)a.n_slots);
-  const size_t lds2 = (size_t)(3 * a.nsps + 1) * sizeof(float);
+  const size_t lds2 = (size_t)a.nsps * sizeof(float4);
   if (a.dtype == FT8_I16)
     hipLaunchKernelGGL(k_sub_apply<int16_t>, g2, dim3(kSubThreads), lds2, s, a);
   else
