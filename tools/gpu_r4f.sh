@@ -19,7 +19,8 @@ DEV=$R/variants/DEV.so
 PYT="python -u -m pytest -v -rP --timeout 300 --timeout-method thread -m gpu"
 FT8HIP_LIB=$MAIN FT8HIP_ALLOW_STALE=1 run digest_main 300 python -u tools/experiments/sub_digest.py
 FT8HIP_LIB=$DEV FT8HIP_ALLOW_STALE=1 run digest_dev 300 python -u tools/experiments/sub_digest.py
-FT8HIP_LIB=$DEV FT8HIP_ALLOW_STALE=1 run devtests 600 $PYT -x tests/test_gpu_tx.py tests/test_gpu_subtract_oracle.py tests/test_gpu_e2e.py tests/test_gpu_stft.py
+FT8HIP_LIB=$DEV FT8HIP_ALLOW_STALE=1 run devtests 600 $PYT -x tests/test_gpu_tx.py tests/test_gpu_subtract_oracle.py tests/test_gpu_e2e.py tests/test_gpu_stft.py tests/test_gpu_stages.py tests/test_gpu_bench_parity.py tests/test_gpu_reftests.py
+run ab 900 python -u tools/ab_variants.py $MAIN $DEV
 for i in 1 2; do
   FT8HIP_LIB=$MAIN FT8HIP_ALLOW_STALE=1 run sub_main$i 300 python -u tools/experiments/sub_bench.py
   FT8HIP_LIB=$DEV FT8HIP_ALLOW_STALE=1 run sub_dev$i 300 python -u tools/experiments/sub_bench.py
