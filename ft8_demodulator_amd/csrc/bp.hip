@@ -22,7 +22,6 @@
 // (two IEEE divisions per edge per iteration, ~30 float64 ops per edge per iteration).
 #include "ft8_internal.h"
 #include "heap_replay.h"
-#include "ft8_bp_layout.h"
 
 namespace ft8 {
 namespace {
@@ -32,11 +31,6 @@ __constant__ uint8_t kEdgeVarD[FT8_LDPC_E] = FT8_EDGE_VAR_INIT;
 __constant__ uint16_t kVarEdgeD[FT8_LDPC_N * 3] = FT8_VAR_EDGE_INIT;
 __constant__ uint8_t kEdgeChkD[FT8_LDPC_E] = FT8_EDGE_CHK_INIT;
 constexpr int kGrayD[8] = {0, 1, 3, 2, 5, 6, 4, 7};  // ft8_decode.py:39
-// lane layout (tools/gen_bp_layout.py): the variable of variable slot (lane, j), its inverse, the
-// row m' of each check -- chosen to cut the variable-major phases' LDS bank conflicts
-__constant__ uint8_t kSlotVarD[192] = FT8_BP_SLOT_VAR_INIT;
-__constant__ uint8_t kVarSlotD[FT8_LDPC_N] = FT8_BP_VAR_SLOT_INIT;
-__constant__ uint8_t kChkRankD[FT8_LDPC_M] = FT8_BP_CHK_RANK_INIT;
 
 constexpr int kEdgeSlots = (FT8_LDPC_E + kWave - 1) / kWave;  // 9
 constexpr int kVarSlots = (FT8_LDPC_N + kWave - 1) / kWave;   // 3
@@ -201,7 +195,7 @@ __device__ __forceinline__ void div_rn(double* q, const double* x, const double*
 // (the workgroup is one lockstep wave), so toc overwrites tov in place and vice versa.
 //
 // Row-position-major layout.  Checks are renumbered degree-7 first (m' = 0..23 the degree-7 rows,
-// 24..82 the degree-6 rows; the order inside each group from ft8_bp_layout.h).  The message of edge (m', q), q being the
+// 24..82 the degree-6 rows, each group in check order).  The message of edge (m', q), q being the
 // edge's position in its check's row (the reference's n_idx, ldpc_decoder.py:85-87, 103-105), lives
 // at index q * 83 + m' (q < 6) or 498 + m' (q = 6, m' < 24); indices 522..583 hold the constant
 // 1.0 that stands in for a degree-6 row's missing seventh factor (1.0 * t == t exactly).  Hence:
@@ -242,15 +236,11 @@ struct WaveLds {
 static_assert(offsetof(WaveLds, msg) == kHdr, "msg follows the header");
 
 // Per-lane tables (registers, built once per wave).
-//   vn:           the variables n_j = kSlotVarD[lane + 64 j] of the lane's variable slots j, 8 bits
-//                 each (255: a padding slot, j = 2 and lanes >= 46)
-//   va[j], vb[j]: variable n_j (variable-major phase): LDS byte addresses of its three edge messages
-//                 in the reference's kFTX_LDPC_Mn order (va, va1, vb)
-//   h[k][j]:      check m' = lane + 64 k (parity): its variables as a 192-bit mask over the variable
-//                 slots, 64-bit word j (lo, hi) -- the parity is popcount(h & hard decisions) from
-//                 wave ballots
+//   va[j], vb[j]: variable n = lane + 64 j (variable-major phase): LDS byte addresses of its three
+//                 edge messages in the reference's kFTX_LDPC_Mn order (va, va1, vb)
+//   h[k][j]:      check m' = lane + 64 k (parity): its variables as a 174-bit mask, 64-bit word j
+//                 (lo, hi) -- the parity is popcount(h & hard decisions) from wave ballots
 struct WaveTables {
-  uint32_t vn;
   uint32_t va[kVarSlots], va1[kVarSlots];
   uint32_t vb[kVarSlots];
   uint32_t h[kChkSlots][kVarSlots][2];
@@ -267,10 +257,13 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
 }
 
 __device__ void load_tables(WaveTables& t, WaveLds& L, int lane) {
-  for (int m = lane; m < FT8_LDPC_M; m += kWave) {  // degree-7 rows first (ft8_bp_layout.h)
-    const int r = kChkRankD[m];
-    L.rank[m] = (uint8_t)r;
-    L.chk_of[r] = (uint8_t)m;
+  if (lane == 0) {  // degree-7 rows first, each group in check order
+    int c7 = 0, c6 = kM7;
+    for (int m = 0; m < FT8_LDPC_M; ++m) {
+      const int r = (kChkStartD[m + 1] - kChkStartD[m]) == 7 ? c7++ : c6++;
+      L.rank[m] = (uint8_t)r;
+      L.chk_of[r] = (uint8_t)m;
+    }
   }
   __syncthreads();
   const uint32_t msg0 = lds_addr(&L.msg[0]);
@@ -278,11 +271,9 @@ __device__ void load_tables(WaveTables& t, WaveLds& L, int lane) {
     const int m = kEdgeChkD[e], q = e - kChkStartD[m], r = L.rank[m];
     return msg0 + 8u * (uint32_t)(q < 6 ? q * kQS + r : kQ6 + r);
   };
-  t.vn = 0;
 #pragma unroll
   for (int j = 0; j < kVarSlots; ++j) {
-    const int n = kSlotVarD[lane + kWave * j];
-    t.vn |= (uint32_t)n << (8 * j);
+    const int n = lane + kWave * j;
     if (n < FT8_LDPC_N) {
       t.va[j] = addr_of(kVarEdgeD[3 * n]);
       t.va1[j] = addr_of(kVarEdgeD[3 * n + 1]);
@@ -301,7 +292,7 @@ __device__ void load_tables(WaveTables& t, WaveLds& L, int lane) {
     if (mp < FT8_LDPC_M) {
       const int m = L.chk_of[mp];
       for (int e = kChkStartD[m]; e < kChkStartD[m + 1]; ++e) {
-        const int v = kVarSlotD[kEdgeVarD[e]];  // the variable's slot: its bit in the ballots
+        const int v = kEdgeVarD[e];
 #pragma unroll
         for (int j = 0; j < kVarSlots; ++j)
 #pragma unroll
@@ -317,7 +308,6 @@ __device__ void load_tables(WaveTables& t, WaveLds& L, int lane) {
   for (int j = 0; j < kVarSlots; ++j) asm volatile("" : "+v"(t.va[j]), "+v"(t.vb[j]));
 #pragma unroll
   for (int j = 0; j < kVarSlots; ++j) asm volatile("" : "+v"(t.va1[j]));
-  asm volatile("" : "+v"(t.vn));
 #pragma unroll
   for (int k = 0; k < kChkSlots; ++k)
 #pragma unroll
@@ -738,7 +728,7 @@ __global__ __launch_bounds__(kWave, kBpLbWaves) void k_bp(BpArgs a) {
     double cv_[kVarSlots];  // codeword[n] (the LLR) of the lane's variables
 #pragma unroll
     for (int j = 0; j < kVarSlots; ++j) {
-      const int n = (tb.vn >> (8 * j)) & 255u;
+      const int n = lane + kWave * j;
       // padding variables (slot 2, lanes >= 46): codeword -1.0, and their three tov read the
       // constant 1.0, so every V->C argument is (-1 + 1) + 1 = 1.0 after the first sweep (-1.0 in
       // it): harmless, never tiny (the wave stays on the short division), never stored
@@ -889,7 +879,7 @@ __global__ __launch_bounds__(kWave, kBpLbWaves) void k_bp(BpArgs a) {
     const bool pack = a.res && min_errors == 0;
     if (a.plain_out || pack) {
 #pragma unroll
-      for (int j = 0; j < kVarSlots; ++j) L.bits[(tb.vn >> (8 * j)) & 255u] = (uint8_t)((hd[j] >> lane) & 1u);
+      for (int j = 0; j < kVarSlots; ++j) L.bits[lane + kWave * j] = (uint8_t)((hd[j] >> lane) & 1u);
       __syncthreads();
     }
     st_cand++;

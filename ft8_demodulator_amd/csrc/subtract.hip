@@ -413,13 +413,9 @@ constexpr int kApList = 1024;                  // overlapping fits listed per pa
 template <typename InT>
 __global__ __launch_bounds__(kSubThreads) void k_sub_apply(SubLaunch a) {
   FT8_RACE_PROLOGUE();
-  // per staged fit and symbol k: (e_{k-1}, e_k, e_{k+1}, phase0[k]) -- the tones whose pulses overlap
-  // symbol k and its start phase -- and the amplitude c = A[k] with the two interpolation slopes
-  // c - A[k-1] and A[k+1] - c (zero at the ends), formed once per fit here rather than per sample
-  // (the same float subtractions: this file is built without contraction)
-  __shared__ float4 s_K[kApFits][tx::kSymbols];
-  __shared__ float4 s_Ac[kApFits][tx::kSymbols];  // (c.x, c.y, (c - A[k-1]).x, .y)
-  __shared__ float2 s_An[kApFits][tx::kSymbols];  // A[k+1] - c
+  __shared__ float s_E[kApFits][tx::kExt];
+  __shared__ float2 s_A[kApFits][tx::kSymbols];
+  __shared__ float s_ph0[kApFits][tx::kSymbols + 1];
   __shared__ long long s_start[kApFits];
   __shared__ float s_f0r[kApFits];
   __shared__ short s_list[kApList];
@@ -435,11 +431,6 @@ __global__ __launch_bounds__(kSubThreads) void k_sub_apply(SubLaunch a) {
   const float fsf = (float)a.fs, inv_nsps = 1.0f / (float)nsps, sr = 6.25f / fsf;
   const int cnt = min(a.counts[slot], a.cap);
   const SubEst* est = reinterpret_cast<const SubEst*>(a.est) + (int64_t)slot * a.cap;
-  // this thread's samples t0 + threadIdx.x + 256 kk, kk < nval, lie inside the slot
-  const int64_t left = a.n_samples - t0 - threadIdx.x;
-  const int nval = left <= 0 ? 0 : (int)min<int64_t>(kApPer, (left + kSubThreads - 1) / kSubThreads);
-  // a step of 256 samples in (symbol, in-symbol offset)
-  const int dk = kSubThreads / nsps, di = kSubThreads - dk * nsps;
   float acc[kApPer];
 #pragma unroll
   for (int k = 0; k < kApPer; ++k) acc[k] = 0.f;
@@ -471,18 +462,20 @@ __global__ __launch_bounds__(kSubThreads) void k_sub_apply(SubLaunch a) {
     for (int b0 = 0; b0 < nl; b0 += kApFits) {
       const int nb = min(kApFits, nl - b0);
       __syncthreads();  // the previous batch is consumed
-      for (int q = threadIdx.x; q < nb * tx::kSymbols; q += kSubThreads) {
-        const int f = q / tx::kSymbols, k = q - f * tx::kSymbols;
+      for (int q = threadIdx.x; q < nb * tx::kExt; q += kSubThreads) {
+        const int f = q / tx::kExt, kk = q - f * tx::kExt;
         const SubEst* e = est + j0 + s_list[b0 + f];
-        // e_{k-1}, e_k, e_{k+1} with the tone sequence held at its ends (the ramps' extension)
-        const float e0 = (float)e->tones[k == 0 ? 0 : k - 1], e1 = (float)e->tones[k];
-        const float e2 = (float)e->tones[k == tx::kSymbols - 1 ? k : k + 1];
-        s_K[f][k] = make_float4(e0, e1, e2, e->phase0[k]);
-        const float cx = e->amp[k][0], cy = e->amp[k][1];
-        const float px = e->amp[k > 0 ? k - 1 : 0][0], py = e->amp[k > 0 ? k - 1 : 0][1];
-        const float nx = e->amp[k < tx::kSymbols - 1 ? k + 1 : k][0], ny = e->amp[k < tx::kSymbols - 1 ? k + 1 : k][1];
-        s_Ac[f][k] = make_float4(cx, cy, cx - px, cy - py);
-        s_An[f][k] = make_float2(nx - cx, ny - cy);
+        const int jj = kk - 1;
+        s_E[f][kk] = (float)e->tones[jj < 0 ? 0 : (jj > tx::kSymbols - 1 ? tx::kSymbols - 1 : jj)];
+      }
+      for (int q = threadIdx.x; q < nb * tx::kSymbols; q += kSubThreads) {
+        const int f = q / tx::kSymbols, kk = q - f * tx::kSymbols;
+        const SubEst* e = est + j0 + s_list[b0 + f];
+        s_A[f][kk] = make_float2(e->amp[kk][0], e->amp[kk][1]);
+      }
+      for (int q = threadIdx.x; q < nb * (tx::kSymbols + 1); q += kSubThreads) {
+        const int f = q / (tx::kSymbols + 1), kk = q - f * (tx::kSymbols + 1);
+        s_ph0[f][kk] = est[j0 + s_list[b0 + f]].phase0[kk];
       }
       if (threadIdx.x < nb) {
         const SubEst* e = est + j0 + s_list[b0 + threadIdx.x];
@@ -493,30 +486,29 @@ __global__ __launch_bounds__(kSubThreads) void k_sub_apply(SubLaunch a) {
       for (int f = 0; f < nb; ++f) {
         const int64_t start = s_start[f];
         const float f0r = s_f0r[f];
+        const float* E = s_E[f];
         const int nr0 = (int)(t0 + threadIdx.x - start);  // |nr0| < 2^31: slots hold < 2^31 samples
         int k = nr0 >= 0 ? nr0 / nsps : -((-nr0 + nsps - 1) / nsps);  // floor
         int i = nr0 - k * nsps;
 #pragma unroll
         for (int kk = 0; kk < kApPer; ++kk) {
-          if ((unsigned)k < (unsigned)tx::kSymbols && kk < nval) {
-            const float4 K = s_K[f][k];
+          const int64_t nabs = t0 + threadIdx.x + (int64_t)kk * kSubThreads;
+          if (k >= 0 && k < tx::kSymbols && nabs < a.n_samples) {
             // the change of G over the symbol's first i samples (tx_device.h's pulse table)
             const float4 dd = s_D[i];
-            const float g = K.x * dd.x + K.y * dd.y + K.z * dd.z;
-            const float cyc = K.w + (float)i * f0r + sr * g;
+            const float g = E[k] * dd.x + E[k + 1] * dd.y + E[k + 2] * dd.z;
+            const float cyc = s_ph0[f][k] + (float)i * f0r + sr * g;
             const float fr = __builtin_amdgcn_fractf(cyc);  // v_sin / v_cos take revolutions
             const float sn = __builtin_amdgcn_sinf(fr), cs = __builtin_amdgcn_cosf(fr);
             const float t = ((float)i + 0.5f) * inv_nsps - 0.5f;  // position from the symbol centre
-            // linear interpolation towards the neighbouring symbol's amplitude
-            const float4 c = s_Ac[f][k];
-            const float2 dn = s_An[f][k];
-            const float sx = t < 0.f ? c.z : dn.x, sy = t < 0.f ? c.w : dn.y;
-            const float2 A = make_float2(c.x + t * sx, c.y + t * sy);
+            const float2 c = s_A[f][k];
+            const float2 o = t < 0.f ? s_A[f][k > 0 ? k - 1 : 0] : s_A[f][k < tx::kSymbols - 1 ? k + 1 : k];
+            const float2 A = t < 0.f ? make_float2(c.x + t * (c.x - o.x), c.y + t * (c.y - o.y))
+                                     : make_float2(c.x + t * (o.x - c.x), c.y + t * (o.y - c.y));
             acc[kk] += ramp_at(k, k * nsps + i, L, nsps) * (A.x * cs - A.y * sn);
           }
-          i += di;
-          k += dk;
-          if (i >= nsps) {
+          i += kSubThreads;
+          while (i >= nsps) {
             i -= nsps;
             ++k;
           }
@@ -529,7 +521,7 @@ __global__ __launch_bounds__(kSubThreads) void k_sub_apply(SubLaunch a) {
 #pragma unroll
   for (int kk = 0; kk < kApPer; ++kk) {
     const int64_t nabs = t0 + threadIdx.x + (int64_t)kk * kSubThreads;
-    if (kk < nval) out[nabs] = ld_sample<InT>(x, nabs) - acc[kk];
+    if (nabs < a.n_samples) out[nabs] = ld_sample<InT>(x, nabs) - acc[kk];
   }
 }
 
