@@ -104,6 +104,8 @@ hipError_t launch_stft(const StftLaunch& a, hipStream_t s);
 // float32 complex arithmetic (stft3840.hip)
 bool stft3840_eligible(const StftLaunch& a);
 hipError_t launch_stft3840(const StftLaunch& a, hipStream_t s);
+bool stftpk_eligible(const StftLaunch& a);        // stft3840.hip: the packed generic real-input plans
+hipError_t launch_stftpk(const StftLaunch& a, hipStream_t s);
 
 // ---- sync score + selection ----------------------------------------------------------------
 // Per (slot, time row) summary written by k_score for k_select: how many grid points of the row

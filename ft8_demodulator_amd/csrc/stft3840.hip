@@ -420,6 +420,154 @@ __global__ __launch_bounds__(kThreads38, 4) void k_stft3840p(Args a) {
   }
 }
 
+// ---- k_stft_pk: the reference's other real-input geometries with packed float32 (round 4) ------
+// The same transform as k_stft_sp (stft.hip) for its compile-time plans -- 20 kHz at bpt = sps = 2
+// (P = 3 200 = 16 x 8 x 5 x 5, the bundled recording's rate), 12 kHz at bpt = sps = 10 (P = 9 600 =
+// 16 x 8 x 15 x 5, the decode test's), 6 kHz (P = 960 = 16 x 4 x 15) -- written with this file's
+// packed complex helpers: one frame per 256-thread workgroup, Stockham stages in place in one padded
+// LDS image (every stage reads its inputs, a barrier, then writes), the first stage a radix-16 DFT
+// of the frame's nonzero half (dft16_half), twiddles W_(Ns R)^(k r) as powers of one table read
+// (radix <= 8; the radix-15 stage reads its 14 from the table: that chain's rounding moved bins 60 dB
+// below a frame's peak past the 1e-3 dB test bound at P = 9 600), the real-input post-twiddle and dB
+// in the epilogue.  k_stft_sp's scalar complex code issued ~7x the VALU instructions per frame of
+// k_stft3840p's packed form for 1.7x the points.
+template <int R>
+__device__ __forceinline__ void dft_r(f2* v) {
+  if constexpr (R == 4) {
+    dft4(v);
+  } else if constexpr (R == 5) {
+    dft5(v);
+  } else if constexpr (R == 8) {
+    dft8(v);
+  } else {
+    static_assert(R == 15, "radix 4, 5, 8 or 15");
+    f2 y[15];
+    dft15(v, y);
+#pragma unroll
+    for (int r = 0; r < 15; ++r) v[r] = y[r];
+  }
+}
+
+struct PkArgs {
+  const void* samples;
+  int64_t slot_stride;
+  int t_lo, f_lo, nf_out, nt_out, hop, nperseg, n_slots, per_xcd;
+  const float* window;
+  float scale;
+  float* out;
+  const f2* tw;    // W_P^m, m in [0, P)
+  const f2* post;  // W_2P^k, k in [0, P]
+};
+
+// one Stockham stage (not the first): butterfly j = t + 256 b of nbf = P / R, Ns = NS
+template <int P, int NS, int R>
+__device__ __forceinline__ void pk_stage(f2* buf, const f2* tw) {
+  constexpr int NBF = P / R, NB = (NBF + kThreads38 - 1) / kThreads38, TSTEP = P / (NS * R);
+  // every index step is a multiple of 16, so pidx(x + 16 m) = pidx(x) + 17 m: one address per
+  // butterfly and immediates (as k_stft3840p)
+  static_assert(NBF % 16 == 0 && NS % 16 == 0, "linear padded index steps");
+  constexpr int RSTEP = NBF + NBF / 16, WSTEP = NS + NS / 16;
+  const int t = threadIdx.x;
+  f2 v[NB][R];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    const int j = t + kThreads38 * b;
+    if (j < NBF) {
+      const int base = pidx(j);
+#pragma unroll
+      for (int r = 0; r < R; ++r) v[b][r] = lds_ld(&buf[base + r * RSTEP]);
+    }
+  }
+  __syncthreads();  // every read of the image is done: write in place
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    const int j = t + kThreads38 * b;
+    if (j < NBF) {
+      const int k = j % NS;
+      if (k != 0) {
+        if constexpr (R <= 8) {
+          const f2 w = tw[k * TSTEP];
+          f2 wr = w;
+#pragma unroll
+          for (int r = 1; r < R; ++r) {
+            v[b][r] = cmul(v[b][r], wr);
+            if (r + 1 < R) wr = cmul(wr, w);
+          }
+        } else {
+#pragma unroll
+          for (int r = 1; r < R; ++r) v[b][r] = cmul(v[b][r], tw[r * k * TSTEP]);
+        }
+      }
+      dft_r<R>(v[b]);
+      const int wbase = pidx((j / NS) * NS * R + k);
+#pragma unroll
+      for (int r = 0; r < R; ++r) lds_st(&buf[wbase + r * WSTEP], v[b][r]);
+    }
+  }
+  __syncthreads();
+}
+
+template <int P, int NS, int R, int... Rest>
+__device__ __forceinline__ void pk_stages(f2* buf, const f2* tw) {
+  pk_stage<P, NS, R>(buf, tw);
+  if constexpr (sizeof...(Rest) > 0) pk_stages<P, NS * R, Rest...>(buf, tw);
+}
+
+template <typename InT, int P, int... Rs>
+__global__ __launch_bounds__(kThreads38) void k_stft_pk(PkArgs a) {
+  FT8_RACE_PROLOGUE();
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_pk[];
+  f2* buf = reinterpret_cast<f2*>(smem_pk);
+  const int t = threadIdx.x;
+  const int nt = a.nt_out;
+  const int rr = (int)(blockIdx.x & 7) * a.per_xcd + (int)(blockIdx.x >> 3);  // XCD-aware, as k_stft
+  if (rr >= nt * a.n_slots) return;
+  const int slot = rr / nt;
+  const int fi = rr - slot * nt;
+  const InT* xs = reinterpret_cast<const InT*>(a.samples) + (int64_t)slot * a.slot_stride + (int64_t)(a.t_lo + fi) * a.hop;
+  // stage 1: radix 16, Ns = 1, over the frame's nonzero half: inputs z[j + r P / 16], r < 8, with
+  // z[n] = (w[2n] x[2n], w[2n+1] x[2n+1]) (zero past nperseg) -> buf[16 j + k]
+  {
+    constexpr int NBF = P / 16, NB = (NBF + kThreads38 - 1) / kThreads38;
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const int j = t + kThreads38 * b;
+      if (j < NBF) {
+        f2 z[8], y[16];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const int n0 = 2 * (j + r * NBF);
+          if (n0 + 1 < a.nperseg) {
+            z[r] = *reinterpret_cast<const f2*>(a.window + n0) * load_pair<InT>(xs, n0);
+          } else {
+            z[r] = f2{n0 < a.nperseg ? a.window[n0] * load_pair<InT>(xs, n0).x : 0.0f, 0.0f};
+          }
+        }
+        dft16_half(z, y);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) lds_st(&buf[17 * j + k], y[k]);  // pidx(16 j + k)
+      }
+    }
+    __syncthreads();
+  }
+  pk_stages<P, 16, Rs...>(buf, a.tw);
+  // epilogue: X[k] = (s - i W_2P^k d) / 2, s = Z[k] + conj Z[P-k], d = Z[k] - conj Z[P-k]
+  constexpr float kDb = 3.0102999566398119521f;  // 10 log10(v) = (10 log10 2) log2(v), v >= 1e-12
+  const float qscale = 0.25f * a.scale;          // |2 X|^2 / 4 / (sum w)^2
+  float* out = a.out + ((int64_t)slot * nt + fi) * a.nf_out;
+  for (int i = t; i < a.nf_out; i += kThreads38) {
+    const int k = a.f_lo + i;
+    const int kk = (k <= P) ? k : 2 * P - k;  // real signal: X[N-k] = conj X[k]
+    const f2 A = lds_ld(&buf[pidx(kk == P ? 0 : kk)]);
+    const f2 B = lds_ld(&buf[pidx(kk == 0 ? 0 : P - kk)]);
+    const f2 sm = add_cj(A, B), df = sub_cj(A, B);
+    const f2 wd = cmul(a.post[kk], df);
+    const f2 X = add_mi(sm, wd);
+    const f2 qq = X * X;
+    out[i] = kDb * __builtin_amdgcn_logf((qq.x + qq.y) * qscale + 1e-12f);
+  }
+}
+
 }  // namespace
 
 bool stft3840_eligible(const StftLaunch& L) {
@@ -452,6 +600,64 @@ hipError_t launch_stft3840(const StftLaunch& L, hipStream_t s) {
     else hipLaunchKernelGGL((k_stft3840p<int16_t, false>), grid, dim3(kThreads38), 0, s, a);
   }
   return hipGetLastError();
+}
+
+// the plans k_stft_pk is built for
+struct PkPlan {
+  int P, n, r[4];
+};
+constexpr PkPlan kPkPlans[] = {{3200, 4, {16, 8, 5, 5}}, {9600, 4, {16, 8, 15, 5}}, {960, 3, {16, 4, 15}}};
+
+static int pk_plan_of(const StftLaunch& L) {
+  if (L.argmax || L.plan.dft || L.plan.blue || !(L.dtype == FT8_F32 || L.dtype == FT8_I16)) return -1;
+  if (L.nfft != 2 * L.plan.P || L.nperseg > L.plan.P || (L.hop % 2) || (L.slot_stride % 2)) return -1;
+  for (int q = 0; q < 3; ++q) {
+    const PkPlan& p = kPkPlans[q];
+    bool ok = L.plan.P == p.P && L.plan.nstages == p.n;
+    for (int i = 0; ok && i < p.n; ++i) ok = L.plan.radix[i] == p.r[i];
+    if (ok) return q;
+  }
+  return -1;
+}
+
+bool stftpk_eligible(const StftLaunch& L) { return pk_plan_of(L) >= 0; }
+
+hipError_t launch_stftpk(const StftLaunch& L, hipStream_t s) {
+  PkArgs a{};
+  a.samples = L.samples;
+  a.slot_stride = L.slot_stride;
+  a.t_lo = L.t_lo;
+  a.f_lo = L.f_lo;
+  a.nf_out = L.f_hi - L.f_lo;
+  a.nt_out = L.t_hi - L.t_lo;
+  a.hop = L.hop;
+  a.nperseg = L.nperseg;
+  a.n_slots = L.n_slots;
+  a.window = reinterpret_cast<const float*>(L.window);
+  a.scale = (float)L.scale;
+  a.out = reinterpret_cast<float*>(L.out);
+  a.tw = reinterpret_cast<const f2*>(L.plan.tw);
+  a.post = reinterpret_cast<const f2*>(L.plan.post);
+  if (a.nt_out <= 0 || a.nf_out <= 0 || L.n_slots <= 0) return hipSuccess;
+  const int q = pk_plan_of(L);
+  if (q < 0) return hipErrorInvalidValue;
+  a.per_xcd = (int)(((int64_t)a.nt_out * L.n_slots + 7) / 8);
+  const dim3 grid((unsigned)(8 * a.per_xcd));
+  const size_t lds = (size_t)(kPkPlans[q].P + kPkPlans[q].P / 16 + 1) * sizeof(f2);
+  auto go = [&](auto kern) {
+    if (lds > 64 * 1024) {
+      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(kern, grid, dim3(kThreads38), lds, s, a);
+    return hipGetLastError();
+  };
+  const bool i16 = L.dtype == FT8_I16;
+  switch (q) {
+    case 0: return i16 ? go(k_stft_pk<int16_t, 3200, 8, 5, 5>) : go(k_stft_pk<float, 3200, 8, 5, 5>);
+    case 1: return i16 ? go(k_stft_pk<int16_t, 9600, 8, 15, 5>) : go(k_stft_pk<float, 9600, 8, 15, 5>);
+    default: return i16 ? go(k_stft_pk<int16_t, 960, 4, 15>) : go(k_stft_pk<float, 960, 4, 15>);
+  }
 }
 
 }  // namespace ft8

@@ -310,9 +310,10 @@ __global__ __launch_bounds__(kSubThreads) void k_sub_est(SubLaunch a) {
   __syncthreads();
 
   // ---- 4. complex amplitude per symbol (one wave per symbol at a time; a lane's samples of the
-  // symbol are loaded kPf at a time before they are used: one round trip per symbol for nsps <= 2048)
+  // symbol are loaded kPf at a time before they are used: two round trips per symbol for nsps <=
+  // 2048; 32 at a time took 211 VGPRs once the ramp left the loop)
   {
-    constexpr int kPf = 32;
+    constexpr int kPf = 16;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const float f0r = (float)(f0 / fs), sr = (float)(6.25 / fs);
     for (int k = wv; k < tx::kSymbols; k += kSubWaves) {
@@ -321,6 +322,24 @@ __global__ __launch_bounds__(kSubThreads) void k_sub_est(SubLaunch a) {
       const int64_t nsym = start + (int64_t)k * nsps;
       const bool inside = nsym >= 0 && nsym + nsps <= a.n_samples;
       const float E0 = (float)s_E[k], E1 = (float)s_E[k + 1], E2 = (float)s_E[k + 2];
+      // the amplitude ramp is 1 except in the first and last symbols (wave-uniform): those take
+      // a plain loop with the ramp, every other symbol the batched loads with rp = 1
+      if (k == 0 || k == tx::kSymbols - 1) {
+#pragma unroll 1
+        for (int i = lane; i < nsps; i += kWave) {
+          const int64_t n = nsym + i;
+          if (!(n >= 0 && n < a.n_samples)) continue;
+          const float rp = ramp_f(k * nsps + i, L, nsps);
+          const float4 dd = s_D[i];
+          const float cyc = ph + (float)i * f0r + sr * (E0 * dd.x + E1 * dd.y + E2 * dd.z);
+          const float fr = __builtin_amdgcn_fractf(cyc);
+          const float sn = __builtin_amdgcn_sinf(fr), cs = __builtin_amdgcn_cosf(fr);
+          const float vr = ld_sample<InT>(x, n) * rp;
+          ax += vr * cs;
+          ay -= vr * sn;
+          rr += rp * rp;
+        }
+      } else
       for (int i0 = lane; i0 < nsps; i0 += kPf * kWave) {
         float v[kPf];
         const InT* xp = x + nsym + i0;
@@ -336,15 +355,15 @@ __global__ __launch_bounds__(kSubThreads) void k_sub_est(SubLaunch a) {
           const int i = i0 + u * kWave;
           const int64_t n = nsym + i;
           if (i >= nsps || !(inside || (n >= 0 && n < a.n_samples))) continue;
-          const float rp = ramp_f(k * nsps + i, L, nsps);
           const float4 dd = s_D[i];  // the change of G over the symbol's first i samples
           const float cyc = ph + (float)i * f0r + sr * (E0 * dd.x + E1 * dd.y + E2 * dd.z);
           const float fr = __builtin_amdgcn_fractf(cyc);  // v_sin / v_cos take revolutions
           const float sn = __builtin_amdgcn_sinf(fr), cs = __builtin_amdgcn_cosf(fr);
-          const float vr = v[u] * rp;
+          // rp = 1: vr = v * 1 and rr += 1 * 1, the same values as the ramped form
+          const float vr = v[u];
           ax += vr * cs;
           ay -= vr * sn;
-          rr += rp * rp;
+          rr += 1.0f;
         }
       }
 #pragma unroll
