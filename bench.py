@@ -471,7 +471,9 @@ def geometry_legs(dev, reps=5):
             "stft_method": {0: "stockham", 1: "packed3840", 2: "chirp-z", 3: "direct DFT"}.get(method, method),
             "score_kernel": "k_score2" if bpt == sps and (bpt <= 4 or bpt == 10) else "k_score",
             "stages_ms": stages,
-            "roofline_stft": {"bound": "hbm", "bytes_per_launch": stft_b, "launch_ms": stages["stft"],
+            "roofline_stft": {"kernel": {"fs20k_bpt2": "k_stft_pk<3200: 16 8 5 5>",
+                                         "fs12k_bpt10": "k_stft_pk<9600: 16 8 15 5>"}.get(name, "k_stft"),
+                              "bound": "hbm", "bytes_per_launch": stft_b, "launch_ms": stages["stft"],
                               "achieved": stft_b / (stages["stft"] * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
                               "unit": "GB/s", "frac": stft_b / (stages["stft"] * 1e-3) / 1e9 / HBM_PEAK_GBS,
                               "bytes": "samples read once (4 B) + dB waterfall written once (4 B per kept bin)"},
