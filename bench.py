@@ -40,6 +40,7 @@ Prints ONE JSON line on rank 0.  Besides the contract fields it carries:
 """
 import argparse
 import json
+import re
 import os
 import sys
 import time
@@ -734,7 +735,10 @@ def counters_for_build(pattern, build_id):
     def _rv(p_):  # rNN[_vK]_... -> (NN, K)
         parts = os.path.basename(p_)[1:].split("_")
         return int(parts[0]), int(parts[1][1:]) if parts[1].startswith("v") and parts[1][1:].isdigit() else -1
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)), key=_rv)
+    # only the headline passes' summaries, r<round>_v<k>_<suffix> (not a leg's, e.g. r4_v23_sub_...)
+    rx = re.compile(r"^r\d+_v\d+_" + re.escape(pattern.split("*_", 1)[1]) + "$")
+    files = sorted((f for f in glob.glob(os.path.join(ROOT, "profiles", pattern)) if rx.match(os.path.basename(f))),
+                   key=_rv)
     for f in reversed(files):
         with open(f) as fh:
             d = json.load(fh)

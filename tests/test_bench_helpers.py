@@ -82,3 +82,20 @@ def test_gather_check_and_shard_sample(bench):
     per = bench.shard_sample(flat, 3, 3)
     assert [len(p) for p in per] == [0, 3, 1]
     assert per[1]["payload"][:, 0].tolist() == [3, 4, 5]
+
+
+def test_counters_for_build_takes_headline_passes_only(tmp_path, monkeypatch):
+    """The headline line's traffic / issue counters come from r<round>_v<k>_pmc*.json of the running
+    build -- never from a leg's summary of the same build (r4_v23_sub_pmc_traffic.json)."""
+    import json
+    import bench
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    for name, bid in (("r4_v23_pmc_traffic.json", "B"), ("r4_v23_sub_pmc_traffic.json", "B"),
+                      ("r4_v22_geo_pmc_traffic.json", "B"), ("r4_v19_pmc_traffic.json", "A")):
+        (prof / name).write_text(json.dumps({"build_id": bid, "kernels": {"k": {"from": name}}}))
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    k, src = bench.counters_for_build("r*_pmc_traffic.json", "B")
+    assert src == "profiles/r4_v23_pmc_traffic.json" and k["k"]["from"] == "r4_v23_pmc_traffic.json"
+    k, src = bench.counters_for_build("r*_pmc_traffic.json", "C")
+    assert k is None and src.startswith("stale: profiles/r4_v23_pmc_traffic.json")
