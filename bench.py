@@ -736,7 +736,7 @@ def counters_for_build(pattern, build_id):
         parts = os.path.basename(p_)[1:].split("_")
         return int(parts[0]), int(parts[1][1:]) if parts[1].startswith("v") and parts[1][1:].isdigit() else -1
     # only the headline passes' summaries, r<round>_v<k>_<suffix> (not a leg's, e.g. r4_v23_sub_...)
-    rx = re.compile(r"^r\d+_v\d+_" + re.escape(pattern.split("*_", 1)[1]) + "$")
+    rx = re.compile(r"^r\d+_v\d+_" + re.escape(pattern.rsplit("*_", 1)[1]) + "$")
     files = sorted((f for f in glob.glob(os.path.join(ROOT, "profiles", pattern)) if rx.match(os.path.basename(f))),
                    key=_rv)
     for f in reversed(files):
