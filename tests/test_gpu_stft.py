@@ -94,3 +94,28 @@ def test_production_stft_ragged_frame_counts(gpu, oracle, frames):
     d = np.abs(spec.astype(np.float64) - ref.astype(np.float64))
     assert d[strong].max() <= 1e-3, d[strong].max()
     assert d.max() <= 0.25, d.max()
+
+
+@pytest.mark.parametrize("fs,bpt,sps", [(20000, 2, 2), (12000, 10, 10), (6000, 2, 2), (12000, 2, 2)])
+def test_int16_stft_equals_float_of_scaled_samples(gpu, fs, bpt, sps):
+    """16-bit PCM into the packed plans (k_stft_pk; k_stft3840p at 12 kHz) reads each sample as
+    float32(x) / 32767 (read_wave_file's scaling): the dB rows equal, bit for bit, those of the float32
+    path given those floats -- the int16 instantiations transform the same values."""
+    from ft8_demodulator_amd import _lib
+    import ctypes
+    n = int(0.16 * fs) * 20
+    nperseg, hop, nfft, T = _lib.geometry(fs, bpt, sps, n)
+    F = nfft // 2
+    rng = np.random.default_rng(fs + bpt)
+    xi = rng.integers(-20000, 20000, size=(2, n)).astype(np.int16)
+    xf = (xi.astype(np.float32) / np.float32(32767.0)).astype(np.float32)
+    ctx = _lib.context()
+    s = gpu.cuda.current_stream().cuda_stream
+    p = _lib.Ft8Params(sample_rate=fs, bins_per_tone=bpt, steps_per_symbol=sps, f_lo=0, f_hi=F, t_lo=0, t_hi=T)
+    out = []
+    for x, code in ((xi, _lib.FT8_I16), (xf, _lib.FT8_F32)):
+        t = gpu.from_numpy(x).cuda()
+        wf = gpu.empty((2, T, F), dtype=gpu.float32, device="cuda")
+        ctx.check(_lib.lib().ft8_stft(ctx.handle, t.data_ptr(), code, n, 2, n, ctypes.byref(p), wf.data_ptr(), s), "stft")
+        out.append(wf.cpu().numpy())
+    assert np.array_equal(out[0], out[1])
