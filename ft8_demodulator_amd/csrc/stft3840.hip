@@ -555,6 +555,21 @@ __global__ __launch_bounds__(kThreads38) void k_stft_pk(PkArgs a) {
   constexpr float kDb = 3.0102999566398119521f;  // 10 log10(v) = (10 log10 2) log2(v), v >= 1e-12
   const float qscale = 0.25f * a.scale;          // |2 X|^2 / 4 / (sum w)^2
   float* out = a.out + ((int64_t)slot * nt + fi) * a.nf_out;
+  if (a.f_lo == 0 && a.nf_out == P) {
+    // every f >= 0 bin kept: bins k and P - k share s and d (k_stft3840p's full-band epilogue):
+    // one pair of LDS reads, one post-twiddle and one packed power for both
+    for (int k = t; k <= P / 2; k += kThreads38) {
+      const f2 A = lds_ld(&buf[pidx(k)]);
+      const f2 B = lds_ld(&buf[pidx(k == 0 ? 0 : P - k)]);
+      const f2 sm = add_cj(A, B), df = sub_cj(A, B);
+      const f2 wd = cmul(a.post[k], df);
+      const f2 re = re_pm(sm, wd), im = im_mp(sm, wd);  // (X1.x, X2.x), (X1.y, -X2.y)
+      const f2 pp = (re * re + im * im) * splat(qscale) + splat(1e-12f);
+      out[k] = kDb * __builtin_amdgcn_logf(pp.x);
+      if (k != 0 && k != P / 2) out[P - k] = kDb * __builtin_amdgcn_logf(pp.y);
+    }
+    return;
+  }
   for (int i = t; i < a.nf_out; i += kThreads38) {
     const int k = a.f_lo + i;
     const int kk = (k <= P) ? k : 2 * P - k;  // real signal: X[N-k] = conj X[k]
