@@ -203,8 +203,11 @@ constexpr int kP = 1920;
 // pass left stages 1 and 3 on 120 / 128 of the 256 threads -- two of the four waves waited at the
 // barrier through the two heaviest stages.
 constexpr int kThreads38 = 256;
-// frames per workgroup (three passes), 31 workgroups per 186-frame slot
-constexpr int kChunk = 6;
+// frames per workgroup (six passes), 16 workgroups per 186-frame slot.  Round 3 measured 6 best
+// (0.171 ms against 0.173-0.176 for 12); with the full-band epilogue in registers (one barrier per
+// pass fewer) 12 is: 0.150 / 0.150 ms against 0.153 / 0.156 for 6, 0.154 for 8, 0.159-0.160 for 4
+// (interleaved, profiles/r4_v29_chunk_ab.log)
+constexpr int kChunk = 12;
 static_assert(kThreads38 == 256 && kChunk % 2 == 0, "two frames per pass on 2 x 128 threads");
 // one LDS image per frame, every stage in place, with pidx padding (stage 1 writes with a
 // 16-complex stride across lanes: 128 B, 32-way bank conflicts unpadded)
