@@ -203,8 +203,11 @@ constexpr int kP = 1920;
 // pass left stages 1 and 3 on 120 / 128 of the 256 threads -- two of the four waves waited at the
 // barrier through the two heaviest stages.
 constexpr int kThreads38 = 256;
-// frames per workgroup (three passes), 31 workgroups per 186-frame slot
-constexpr int kChunk = 6;
+// frames per workgroup (six passes), 16 workgroups per 186-frame slot.  Round 3 measured 6 best
+// (0.171 ms against 0.173-0.176 for 12); with the full-band epilogue in registers (one barrier per
+// pass fewer) 12 is: 0.150 / 0.150 ms against 0.153 / 0.156 for 6, 0.154 for 8, 0.159-0.160 for 4
+// (interleaved, profiles/r4_v29_chunk_ab.log)
+constexpr int kChunk = 12;
 static_assert(kThreads38 == 256 && kChunk % 2 == 0, "two frames per pass on 2 x 128 threads");
 // one LDS image per frame, every stage in place, with pidx padding (stage 1 writes with a
 // 16-complex stride across lanes: 128 B, 32-way bank conflicts unpadded)
@@ -555,6 +558,21 @@ __global__ __launch_bounds__(kThreads38) void k_stft_pk(PkArgs a) {
   constexpr float kDb = 3.0102999566398119521f;  // 10 log10(v) = (10 log10 2) log2(v), v >= 1e-12
   const float qscale = 0.25f * a.scale;          // |2 X|^2 / 4 / (sum w)^2
   float* out = a.out + ((int64_t)slot * nt + fi) * a.nf_out;
+  if (a.f_lo == 0 && a.nf_out == P) {
+    // every f >= 0 bin kept: bins k and P - k share s and d (k_stft3840p's full-band epilogue):
+    // one pair of LDS reads, one post-twiddle and one packed power for both
+    for (int k = t; k <= P / 2; k += kThreads38) {
+      const f2 A = lds_ld(&buf[pidx(k)]);
+      const f2 B = lds_ld(&buf[pidx(k == 0 ? 0 : P - k)]);
+      const f2 sm = add_cj(A, B), df = sub_cj(A, B);
+      const f2 wd = cmul(a.post[k], df);
+      const f2 re = re_pm(sm, wd), im = im_mp(sm, wd);  // (X1.x, X2.x), (X1.y, -X2.y)
+      const f2 pp = (re * re + im * im) * splat(qscale) + splat(1e-12f);
+      out[k] = kDb * __builtin_amdgcn_logf(pp.x);
+      if (k != 0 && k != P / 2) out[P - k] = kDb * __builtin_amdgcn_logf(pp.y);
+    }
+    return;
+  }
   for (int i = t; i < a.nf_out; i += kThreads38) {
     const int k = a.f_lo + i;
     const int kk = (k <= P) ? k : 2 * P - k;  // real signal: X[N-k] = conj X[k]

@@ -77,9 +77,9 @@ def test_any_fft_length_matches_scipy(gpu, oracle, fs, bpt, sps, cplx, dt, metho
     assert d.max() <= loose, d.max()
 
 
-@pytest.mark.parametrize("frames", [1, 2, 3, 5, 6, 7, 11, 13])
+@pytest.mark.parametrize("frames", [1, 2, 3, 5, 6, 7, 11, 12, 13, 23, 25])
 def test_production_stft_ragged_frame_counts(gpu, oracle, frames):
-    """k_stft3840p transforms two frames per pass in runs of 6: runs that end on an odd frame (the
+    """k_stft3840p transforms two frames per pass in runs of 12: runs that end on an odd frame (the
     second frame of the last pass absent) and runs shorter than a chunk match scipy like full ones."""
     from ft8_demodulator_amd import _lib, calculate_spectrogram
     fs, n = 12000, (frames - 1) * 960 + 1920
