@@ -726,6 +726,21 @@ REFERENCE_MEASURED = {
 STAGE_ORDER = ("stft", "score", "select", "llr", "bp", "compact")
 
 
+def gpu_clock_ghz(device=0):
+    """The shader clock this box runs kernels at (tools/probe/clock.hip: clock64 cycles over the
+    constant-rate wall clock while one wave spins), or None.  Boxes differ: the same build's k_bp
+    takes the same cycles at 1.8-2.1 GHz ("Boxes and clocks")."""
+    import ctypes
+    try:
+        lib = ctypes.CDLL(os.path.join(ROOT, "tools", "probe", "libclockprobe.so"))
+        fn = lib.ft8probe_clock_ghz
+        fn.argtypes, fn.restype = [ctypes.c_int, ctypes.POINTER(ctypes.c_double)], ctypes.c_int
+        g = ctypes.c_double(0.0)
+        return round(g.value, 3) if fn(int(device), ctypes.byref(g)) == 0 and g.value > 0 else None
+    except OSError:
+        return None
+
+
 def counters_for_build(pattern, build_id):
     """The newest committed profiles/<pattern> summary whose build_id equals the running library's
     -> (kernels dict, relative path); (None, "stale: <newest file> (build <id>)") when none matches,
@@ -1157,6 +1172,8 @@ def main():
         "parity": parity,
         "reference_measured": REFERENCE_MEASURED,
         "build_id": build_id,
+        # the shader clock of this box, measured after the timed work (boxes differ by up to ~15 %)
+        "gpu_clock_ghz": gpu_clock_ghz(local),
     }
     if gather is not None:
         line["gather"] = gather
