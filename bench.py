@@ -727,18 +727,22 @@ STAGE_ORDER = ("stft", "score", "select", "llr", "bp", "compact")
 
 
 def gpu_clock_ghz(device=0):
-    """The shader clock this box runs kernels at (tools/probe/clock.hip: clock64 cycles over the
-    constant-rate wall clock while one wave spins), or None.  Boxes differ: the same build's k_bp
-    takes the same cycles at 1.8-2.1 GHz ("Boxes and clocks")."""
+    """The shader clock of this box (tools/probe/clock.hip: clock64 cycles over the constant-rate
+    wall clock): {"light": one wave spinning, "loaded": four FP64-FMA waves per SIMD on every CU,
+    k_bp's issue load} in GHz, or None.  Boxes differ: the same build's k_bp takes the same cycles at
+    1.8-2.1 GHz ("Boxes and clocks")."""
     import ctypes
     try:
         lib = ctypes.CDLL(os.path.join(ROOT, "tools", "probe", "libclockprobe.so"))
-        fn = lib.ft8probe_clock_ghz
-        fn.argtypes, fn.restype = [ctypes.c_int, ctypes.POINTER(ctypes.c_double)], ctypes.c_int
-        g = ctypes.c_double(0.0)
-        return round(g.value, 3) if fn(int(device), ctypes.byref(g)) == 0 and g.value > 0 else None
     except OSError:
         return None
+    fn = lib.ft8probe_clock_ghz
+    fn.argtypes, fn.restype = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double)], ctypes.c_int
+    out = {}
+    for name, loaded in (("light", 0), ("loaded", 1)):
+        g = ctypes.c_double(0.0)
+        out[name] = round(g.value, 3) if fn(int(device), loaded, ctypes.byref(g)) == 0 and g.value > 0 else None
+    return out
 
 
 def counters_for_build(pattern, build_id):
