@@ -122,21 +122,26 @@ int ensure(ft8_ctx* c, DevBuf& b, size_t bytes);
 
 // ensure() for a buffer that must read as zeros when (re)allocated: the k_bp work counters, which
 // every k_bp launch leaves at 0 again (bp.hip), so they are cleared only here
-int ensure_zeroed(ft8_ctx* c, DevBuf& b, size_t bytes, hipStream_t s) {
+// *reallocated (optional) reports whether the buffer was (re)allocated and zeroed; a grown buffer
+// can come back at the old address, so the test is the capacity as well as the pointer
+int ensure_zeroed(ft8_ctx* c, DevBuf& b, size_t bytes, hipStream_t s, bool* reallocated = nullptr) {
   void* old = b.p;
   const size_t old_cap = b.cap;
+  if (reallocated) *reallocated = false;
   int rc = ensure(c, b, bytes);
   if (rc || (b.p == old && b.cap == old_cap)) return rc;
+  if (reallocated) *reallocated = true;
   hipError_t e = hipMemsetAsync(b.p, 0, b.cap, s);
   return e == hipSuccess ? FT8_OK : hipfail(c, e, "memset");
 }
 
-// the k_bp claim counters (8 B each) and their host-side ticket bases
+// the k_bp claim counters (8 B each) and their host-side ticket bases: whenever the counters are
+// (re)allocated they read 0, so every base restarts at 0 and the vector covers the new capacity
 int ensure_work(ft8_ctx* c, int n_counters, hipStream_t s) {
-  void* old = c->work.p;
-  int rc = ensure_zeroed(c, c->work, sizeof(unsigned long long) * (size_t)n_counters, s);
+  bool fresh = false;
+  int rc = ensure_zeroed(c, c->work, sizeof(unsigned long long) * (size_t)n_counters, s, &fresh);
   if (rc) return rc;
-  if (c->work.p != old) c->work_base.assign(c->work.cap / sizeof(unsigned long long), 0ull);
+  if (fresh) c->work_base.assign(c->work.cap / sizeof(unsigned long long), 0ull);
   return FT8_OK;
 }
 

@@ -18,10 +18,16 @@ constexpr int kWave = 64;
 // the workgroup (rotating with the workgroup id) sleeps ~64 k cycles before it starts.  A read of
 // another wave's LDS staging that no barrier orders after the write then sees the sentinel instead
 // of a late value, deterministically, and the GPU tests fail.
+// tools/probe/race_control.hip is the positive control: a kernel with a deliberately missing
+// barrier that must read the sentinel under this prologue (tests/test_gpu_race_control.py).
 #ifdef FT8_RACE_CHECK
+}  // namespace ft8
+#include <hsa/hsa.h>
+namespace ft8 {
+static_assert(offsetof(hsa_kernel_dispatch_packet_t, group_segment_size) == 28, "dispatch packet layout");
 __device__ __forceinline__ void race_prologue() {
-  const char* dp = (const char*)__builtin_amdgcn_dispatch_ptr();
-  const uint32_t bytes = *(const uint32_t*)(dp + 20);  // hsa_kernel_dispatch_packet_t.group_segment_size
+  const auto* pkt = (const hsa_kernel_dispatch_packet_t*)__builtin_amdgcn_dispatch_ptr();
+  const uint32_t bytes = pkt->group_segment_size;  // static + dynamic LDS of this workgroup
   const uint32_t nt = blockDim.x * blockDim.y * blockDim.z;
   const uint32_t t = threadIdx.x + blockDim.x * (threadIdx.y + blockDim.y * threadIdx.z);
   for (uint32_t off = 4 * t; off + 4 <= bytes; off += 4 * nt)

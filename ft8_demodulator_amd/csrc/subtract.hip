@@ -566,6 +566,14 @@ __global__ __launch_bounds__(kWave) void k_merge(ft8_result* out, int32_t* count
 
 size_t sub_est_bytes() { return sizeof(SubEst); }
 
+// dynamic LDS above the default 64 KB needs the kernel's attribute raised first (the pulse table is
+// nsps float4s: 61.4 KB at 24 kHz, more above)
+template <typename K>
+static hipError_t allow_lds(K kern, size_t dyn) {
+  if (dyn <= 32 * 1024) return hipSuccess;  // + static LDS: stay clear of the 64 KB default
+  return hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
+}
+
 hipError_t launch_sub_est(const SubLaunch& a, hipStream_t s) {
   if (a.n_slots <= 0 || a.n_samples <= 0) return hipSuccess;
   if (a.Q <= 0 || a.Q > kMaxQ || a.nsps % a.Q != 0 || a.hop <= 0 || a.nsps % a.hop != 0) return hipErrorInvalidValue;
@@ -577,12 +585,21 @@ hipError_t launch_sub_est(const SubLaunch& a, hipStream_t s) {
     const unsigned grid_rest = (unsigned)(((a.n_slots + 7) / 8) * 8 * (int64_t)kSubRestStride);
     const size_t mz = (size_t)tx::kSymbols * a.Q + 2 * (a.Q / (2 * (a.nsps / a.hop)) + 2);
     const size_t lds = std::max(mz * sizeof(float2), (size_t)a.nsps * sizeof(float4));
+    hipError_t e = hipSuccess;
     if (a.dtype == FT8_I16) {
+      if ((e = allow_lds(k_sub_est<int16_t, false>, lds)) != hipSuccess) return e;
       hipLaunchKernelGGL((k_sub_est<int16_t, false>), dim3(grid), dim3(kSubThreads), lds, s, a);
-      if (a.cap > kSubRecStride) hipLaunchKernelGGL((k_sub_est<int16_t, true>), dim3(grid_rest), dim3(kSubThreads), lds, s, a);
+      if (a.cap > kSubRecStride) {
+        if ((e = allow_lds(k_sub_est<int16_t, true>, lds)) != hipSuccess) return e;
+        hipLaunchKernelGGL((k_sub_est<int16_t, true>), dim3(grid_rest), dim3(kSubThreads), lds, s, a);
+      }
     } else {
+      if ((e = allow_lds(k_sub_est<float, false>, lds)) != hipSuccess) return e;
       hipLaunchKernelGGL((k_sub_est<float, false>), dim3(grid), dim3(kSubThreads), lds, s, a);
-      if (a.cap > kSubRecStride) hipLaunchKernelGGL((k_sub_est<float, true>), dim3(grid_rest), dim3(kSubThreads), lds, s, a);
+      if (a.cap > kSubRecStride) {
+        if ((e = allow_lds(k_sub_est<float, true>, lds)) != hipSuccess) return e;
+        hipLaunchKernelGGL((k_sub_est<float, true>), dim3(grid_rest), dim3(kSubThreads), lds, s, a);
+      }
     }
     return hipGetLastError();
   }
@@ -593,10 +610,14 @@ hipError_t launch_sub_apply(const SubLaunch& a, hipStream_t s) {
   if (a.n_slots <= 0 || a.n_samples <= 0) return hipSuccess;
   dim3 g2((unsigned)((a.n_samples + kApTile - 1) / kApTile), (unsigned)a.n_slots);
   const size_t lds2 = (size_t)a.nsps * sizeof(float4);
-  if (a.dtype == FT8_I16)
+  hipError_t e = hipSuccess;
+  if (a.dtype == FT8_I16) {
+    if ((e = allow_lds(k_sub_apply<int16_t>, lds2)) != hipSuccess) return e;
     hipLaunchKernelGGL(k_sub_apply<int16_t>, g2, dim3(kSubThreads), lds2, s, a);
-  else
+  } else {
+    if ((e = allow_lds(k_sub_apply<float>, lds2)) != hipSuccess) return e;
     hipLaunchKernelGGL(k_sub_apply<float>, g2, dim3(kSubThreads), lds2, s, a);
+  }
   return hipGetLastError();
 }
 

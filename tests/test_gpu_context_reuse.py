@@ -1,0 +1,66 @@
+"""One libft8hip context across entry points whose scratch needs differ.
+
+The k_bp claim counters live in one context buffer: [0] for ft8_bp, [1 + k] for decode chunk k,
+each with a host-side ticket base.  When a later call needs more counters the buffer is
+reallocated and zeroed (possibly at the same address), so every base must restart at 0 and the
+base vector must grow with it; otherwise k_bp retires every wave at once (no decodes, no error) or
+writes past the base vector.  Sequence on a fresh context: ft8_bp -> a decode cut into one-slot
+chunks (n_slots + 1 counters) -> ft8_bp -> a one-chain decode, each checked against the oracle or
+the one-chain decode of a separate context."""
+import ctypes
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+KW = dict(max_candidates=300, min_score=2, max_iterations=20)
+
+
+def _bp(ctx, llr, iters):
+    import torch
+    from ft8_demodulator_amd import _lib
+    a = torch.from_numpy(np.ascontiguousarray(llr, dtype=np.float64)).cuda()
+    n = a.shape[0]
+    plain = torch.zeros(n, 174, dtype=torch.uint8, device="cuda")
+    res = torch.zeros(n * _lib.RESULT_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
+    ctx.check(_lib.lib().ft8_bp(ctx.handle, _lib.ptr(a), n, int(iters), _lib.ptr(plain), _lib.ptr(res),
+                                _lib.stream_handle()), "ft8_bp")
+    return plain.cpu().numpy(), res.cpu().numpy().view(_lib.RESULT_DTYPE)
+
+
+def test_counters_survive_reallocation(gpu, oracle):
+    from ft8_demodulator_amd import _lib, synth
+    from ft8_demodulator_amd._pipeline import SlotDecoder
+    rng = np.random.default_rng(11)
+    llr = rng.standard_normal((96, 174)) * 2.5
+    want = [oracle.bp_decode(v, 20) for v in llr]
+
+    def check_bp(ctx):
+        plain, rec = _bp(ctx, llr, 20)
+        for i, (p_ref, e_ref) in enumerate(want):
+            assert int(rec[i]["ldpc_errors"]) == e_ref and np.array_equal(plain[i], p_ref), i
+
+    x, _ = synth.make_slots(12, 50, seed=5150, device="cuda")
+    ref = SlotDecoder(12000, 2, 2, **KW)
+    ref.ctx = _lib.Context(0)
+    want_recs = [r.tobytes() for r in ref.records(x)]
+    assert sum(len(r) for r in want_recs) > 0
+
+    ctx = _lib.Context(0)                       # fresh: one counter after the first ft8_bp
+    check_bp(ctx)
+    check_bp(ctx)                               # the base advanced: the second launch decodes too
+    dec = SlotDecoder(12000, 2, 2, **KW)
+    dec.ctx = ctx
+    ctx.set_pipeline(chunk_slots=1, n_streams=2)  # 12 chunks: 13 counters, the buffer is reallocated
+    try:
+        got = [r.tobytes() for r in dec.records(x)]
+        assert got == want_recs
+        check_bp(ctx)
+        got = [r.tobytes() for r in dec.records(x)]
+        assert got == want_recs
+    finally:
+        ctx.set_pipeline(0, 0, 2)
+    got = [r.tobytes() for r in dec.records(x)]   # one chain again, on the grown buffer
+    assert got == want_recs
+    check_bp(ctx)
