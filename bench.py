@@ -826,7 +826,12 @@ def launch_ranks(args):
     import socket
     import subprocess
     import torch
-    n_dev = torch.cuda.device_count()  # does not initialise HIP on this image
+    n_dev = torch.cuda.device_count()  # does not initialise HIP on this image (asserted below)
+    # the ranks are started as child processes; a parent that had initialised the GPU must not
+    # spawn them (exec from a GPU-initialised process is forbidden on this pool)
+    if torch.cuda.is_initialized():
+        print("bench.py: the launcher process initialised HIP before spawning its ranks", file=sys.stderr)
+        return 2
     if n_dev < (1 if args.share_gpu else args.gpus):
         print(f"bench.py: --gpus {args.gpus} requested but only {n_dev} GPU(s) are visible", file=sys.stderr)
         return 2
@@ -903,9 +908,7 @@ def main():
     sub_oracle = None
     if rank == 0 and world == 1 and not args.no_cpu and not args.no_subtract and args.subtract_oracle_slots > 0:
         sub_oracle = subtract_oracle(args.subtract_oracle_slots, host_cores()[0])
-    if False:
-        pass
-    elif world > 1 and args.shard_parity_slots > 0:
+    if world > 1 and args.shard_parity_slots > 0:
         # every rank: the oracle decodes the first slots of this rank's own shard (global seeds
         # 100000 + g) on its share of the host cores, before the GPU is touched; those bytes are
         # the first rows of the rank's batch, so the gathered records of the last timed step are
@@ -968,13 +971,19 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    # one HIP event after every timed step (recorded on the stream, no host sync): the per-step GPU
+    # periods show whether the timed steps had settled (k_bp's clock ramps over its first launches)
+    step_ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    step_ev[0].record()
+    for i_ in range(args.steps):
         counts = step(keep=True)
+        step_ev[i_ + 1].record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    step_ms = [step_ev[i_].elapsed_time(step_ev[i_ + 1]) for i_ in range(args.steps)]
     decoded = int(counts.sum().item())
     gather = None
     gather_last = None
@@ -1004,6 +1013,7 @@ def main():
         ctx.timing(reset=True)
         if st == "bp":
             ctx.counters(reset=True)
+            ctx.bp_clock(reset=True)
         ctx.set_timing(True, stages=[st])
         for _ in range(R):
             step()
@@ -1013,6 +1023,7 @@ def main():
         stage_ms[st] = tm[0] / max(tm[1], 1)
         if st == "bp":
             cn = ctx.counters(reset=True)
+            bclk = ctx.bp_clock(reset=True)
     ctx.set_timing(False, stages=None)
     # the STFT is the first kernel of a step, so an event placed before it also times the host's
     # launch gap; its launch duration comes from back-to-back re-launches of the step's STFT instead
@@ -1073,6 +1084,29 @@ def main():
     # algorithmic bytes per slot; slots/s x B_slot vs the 8 TB/s HBM peak
     b_slot = x.shape[1] * 4 + 2 * plan.F * plan.T * 4 + kw["max_candidates"] * (58 * 8 * 4 + 174 * 8 * 2 + 40)
     step_gbs = value / world * b_slot / 1e9
+
+    # k_bp's own clock (ft8_get_bp_clock, the same R launches the events timed): every persistent
+    # wave reads the shader-clock and wall-clock counters at start and retire.  Cycles per launch do
+    # not depend on the box's clock; cycles / wall time is the clock k_bp itself ran at, so a change
+    # of k_bp time between lines splits into "more cycles" or "lower clock" from the line alone
+    bp_clock = None
+    if bclk["waves"] and bclk["wave_wall_ticks"] and bclk["wall_clock_khz"]:
+        waves_per_launch = bclk["waves"] / R
+        mean_wave_cycles = bclk["wave_cycles"] / bclk["waves"]
+        bp_clock = {"mean_wave_cycles": mean_wave_cycles, "max_wave_cycles": bclk["max_wave_cycles"],
+                    "waves_per_launch": waves_per_launch,
+                    "effective_ghz": bclk["wave_cycles"] / (bclk["wave_wall_ticks"] / (bclk["wall_clock_khz"] * 1e3)) / 1e9,
+                    "cycles_per_event_ms_ghz": mean_wave_cycles / (bp_ms * 1e-3) / 1e9,
+                    "wave_busy_vs_event": (bclk["wave_wall_ticks"] / bclk["waves"] / (bclk["wall_clock_khz"] * 1e3))
+                    / (bp_ms * 1e-3),
+                    "note": "mean_wave_cycles ~ k_bp's cycles per launch (persistent waves live for the launch); "
+                            "effective_ghz = summed wave cycles / summed wave wall time; wave_busy_vs_event = mean "
+                            "wave lifetime / event-timed launch"}
+    q1 = max(1, K // 4)
+    step_times = {"ms": [round(v_, 4) for v_ in step_ms],
+                  "first_quarter_mean_ms": sum(step_ms[:q1]) / q1, "last_quarter_mean_ms": sum(step_ms[-q1:]) / q1,
+                  "from": "HIP events between consecutive timed steps (GPU periods; the line's ms_per_step is the "
+                          "host wall clock around all of them)"}
 
     stress = None
     if world == 1 and not args.no_bp_stress:
@@ -1153,7 +1187,8 @@ def main():
                      "flops_per_launch": flops, "launch_ms": bp_ms,
                      "launch_ms_from": f"HIP events around k_bp alone in {R} full steps after the timed loop",
                      "bp_passes_per_launch": cn["passes"] / R, "candidates_per_launch": cn["candidates"] / R,
-                     "issue": issue},
+                     "clock": bp_clock, "issue": issue},
+        "step_times": step_times,
         "step_hbm": {"what": "BASELINE.md whole-step accounting: slots/s per GPU x B_slot algorithmic bytes "
                              "(the step is FP64-VALU bound in k_bp, so this fraction is low by construction)",
                      "bytes_per_slot": b_slot, "achieved": step_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",

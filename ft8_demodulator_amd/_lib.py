@@ -123,6 +123,7 @@ def lib():
             "ft8_set_timing": ([vp, ctypes.c_int], ctypes.c_int),
             "ft8_get_timing": ([vp, vp, vp, ctypes.c_int], ctypes.c_int),
             "ft8_get_counters": ([vp, vp, ctypes.c_int], ctypes.c_int),
+            "ft8_get_bp_clock": ([vp, vp, ctypes.c_int], ctypes.c_int),
             "ft8_set_pipeline": ([vp, i32, i32, i32], ctypes.c_int),
             "ft8_encode": ([vp, vp, i32, i32, vp, vp, vp, vp], ctypes.c_int),
             "ft8_synthesize": ([vp, vp, vp, i32, i32, i32, vp, ctypes.c_int, i64, i32, i64, vp], ctypes.c_int),
@@ -180,7 +181,7 @@ def source_hash():
 EXPORTED_SYMBOLS = (
     "ft8_create", "ft8_destroy", "ft8_last_error", "ft8_abi_version", "ft8_limits", "ft8_geometry",
     "ft8_stft", "ft8_sync_select", "ft8_llr", "ft8_normalize", "ft8_bp", "ft8_decode_batch", "ft8_select_warnings",
-    "ft8_crc14", "ft8_ldpc_check", "ft8_set_timing", "ft8_get_timing", "ft8_get_counters", "ft8_set_pipeline",
+    "ft8_crc14", "ft8_ldpc_check", "ft8_set_timing", "ft8_get_timing", "ft8_get_counters", "ft8_get_bp_clock", "ft8_set_pipeline",
     "ft8_encode", "ft8_synthesize", "ft8_subtract", "ft8_stft_argmax", "ft8_drift_fit", "ft8_drift_correct",
     "ft8_build_id", "ft8_build_flags", "ft8_replay_stage", "ft8_set_timing_stages", "ft8_sync_score",
     "ft8_pack_bytes", "ft8_pack_decodes", "ft8_subtract_fits", "ft8_stft_method", "ft8_stft_screen_stats")
@@ -262,6 +263,14 @@ class Context:
         v = (ctypes.c_int64 * 4)()
         self.check(lib().ft8_get_counters(self.handle, v, int(reset)), "ft8_get_counters")
         return {"candidates": v[0], "iterations": v[1], "passes": v[2], "converged": v[3]}
+
+    def bp_clock(self, reset: bool = False):
+        """ft8_get_bp_clock: k_bp's waves' own shader-clock cycles and wall-clock time, summed over
+        the launches made while timing was enabled."""
+        v = (ctypes.c_int64 * 5)()
+        self.check(lib().ft8_get_bp_clock(self.handle, v, int(reset)), "ft8_get_bp_clock")
+        return {"wave_cycles": v[0], "wave_wall_ticks": v[1], "max_wave_cycles": v[2], "waves": v[3],
+                "wall_clock_khz": v[4]}
 
     def __del__(self):
         try:

@@ -329,6 +329,8 @@ struct BpArgs {
   unsigned long long* work;   // claim counter (64-bit, never reset)
   unsigned long long work_base;  // this launch's first ticket (BpLaunch.work_base)
   unsigned long long* stats;  // nullable: [candidates, iterations entered, message passes, converged]
+  unsigned long long* clock;  // nullable (timed launches only): [sum of wave shader-clock cycles,
+                              //  sum of wave wall-clock ticks, max wave cycles, waves] (ft8_get_bp_clock)
   int slot0;
   int tie_blocks;             // k_llr's first tie_blocks workgroups run tie_order
   TieArgs tie;
@@ -687,6 +689,9 @@ __device__ __forceinline__ void check_products(double* x, uint32_t la, int lane)
 // modes: 0 per-slot candidate lists (records carry slot / abs_time / abs_freq / score), 2 plain LLRs
 template <bool NANSAFE>
 __global__ __launch_bounds__(kWave, kBpLbWaves) void k_bp(BpArgs a) {
+  // the wave's lifetime in shader-clock cycles and constant-rate wall-clock ticks (counter pass
+  // only): cycles per launch are clock-independent, cycles / wall time is the clock the kernel ran at
+  const unsigned long long clk0 = a.clock ? clock64() : 0ull, wall0 = a.clock ? wall_clock64() : 0ull;
   __shared__ WaveLds L;
   const int lane = threadIdx.x;
   WaveTables tb;
@@ -951,6 +956,13 @@ __global__ __launch_bounds__(kWave, kBpLbWaves) void k_bp(BpArgs a) {
     atomicAdd(&a.stats[2], (unsigned long long)st_pass);
     atomicAdd(&a.stats[3], (unsigned long long)st_conv);
   }
+  if (a.clock && lane == 0) {
+    const unsigned long long cyc = clock64() - clk0, wall = wall_clock64() - wall0;
+    atomicAdd(&a.clock[0], cyc);
+    atomicAdd(&a.clock[1], wall);
+    atomicMax(&a.clock[2], cyc);
+    atomicAdd(&a.clock[3], 1ull);
+  }
 }
 
 // one wave per slot: successes in candidate order -> out[slot][0..cap), counts[slot]
@@ -1104,6 +1116,7 @@ BpArgs make_args(const BpLaunch& L) {
   a.work = L.work;
   a.work_base = L.work_base ? *L.work_base : 0ull;
   a.stats = L.stats;
+  a.clock = L.clock;
   a.slot0 = L.slot0;
   a.tie = TieArgs{L.n_slots, L.N, L.cand_count, L.warn, L.tie, L.cand_score};
   a.tie_blocks = (L.tie && L.mode == 0) ? (L.n_slots + 7) / 8 * 8 : 0;

@@ -705,6 +705,7 @@ int decode_pass(ft8_ctx* c, const void* d_samples, int dtype, int64_t n_samples,
     B.work = (unsigned long long*)c->work.p + 1 + k;
     B.work_base = &c->work_base[1 + k];
     B.stats = (unsigned long long*)c->stats.p;
+    B.clock = c->timing && c->stats.p ? (unsigned long long*)c->stats.p + 4 : nullptr;
     B.grid_waves = n_str > 0 ? c->bp_waves : 8;  // clamped to the kernel's 4 resident waves per SIMD
     B.tie = tie;
     B.warn = warn;
@@ -1170,6 +1171,7 @@ int ft8_bp(ft8_ctx* c, const double* d_llr, int32_t n, int32_t max_iterations, u
   L.work = (unsigned long long*)c->work.p;
   L.work_base = &c->work_base[0];
   L.stats = (unsigned long long*)c->stats.p;
+  L.clock = c->timing && c->stats.p ? (unsigned long long*)c->stats.p + 4 : nullptr;
   StageTimer tm(c, 3, (hipStream_t)stream);
   hipError_t e = launch_bp(L, (hipStream_t)stream);
   tm.done();
@@ -1489,9 +1491,9 @@ int ft8_set_timing(ft8_ctx* c, int enable) {
   c->timing = enable != 0;
   if (c->timing && !c->stats.p) {
     DeviceGuard dg(c->device);
-    int rc = ensure(c, c->stats, 4 * sizeof(unsigned long long));
+    int rc = ensure(c, c->stats, 8 * sizeof(unsigned long long));
     if (rc) return rc;
-    hipError_t e = hipMemset(c->stats.p, 0, 4 * sizeof(unsigned long long));
+    hipError_t e = hipMemset(c->stats.p, 0, 8 * sizeof(unsigned long long));
     if (e != hipSuccess) return hipfail(c, e, "stats reset");
   }
   return FT8_OK;
@@ -1514,6 +1516,25 @@ int ft8_get_counters(ft8_ctx* c, int64_t* out4, int reset) {
   if (e == hipSuccess && reset) e = hipMemset(c->stats.p, 0, sizeof(v));
   if (e != hipSuccess) return hipfail(c, e, "counters");
   for (int i = 0; i < 4; ++i) out4[i] = (int64_t)v[i];
+  return FT8_OK;
+}
+
+int ft8_get_bp_clock(ft8_ctx* c, int64_t* out5, int reset) {
+  if (!c || !out5) return FT8_E_ARG;
+  for (int i = 0; i < 5; ++i) out5[i] = 0;
+  DeviceGuard dg(c->device);
+  int khz = 0;
+  hipError_t e = hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->device);
+  if (e != hipSuccess) return hipfail(c, e, "wall clock rate");
+  out5[4] = khz;
+  if (!c->stats.p) return FT8_OK;
+  unsigned long long v[4];
+  e = hipDeviceSynchronize();
+  unsigned long long* clk = (unsigned long long*)c->stats.p + 4;
+  if (e == hipSuccess) e = hipMemcpy(v, clk, sizeof(v), hipMemcpyDeviceToHost);
+  if (e == hipSuccess && reset) e = hipMemset(clk, 0, sizeof(v));
+  if (e != hipSuccess) return hipfail(c, e, "bp clock");
+  for (int i = 0; i < 4; ++i) out5[i] = (int64_t)v[i];
   return FT8_OK;
 }
 

@@ -207,6 +207,7 @@ struct BpLaunch {
   unsigned long long* work;
   unsigned long long* work_base;
   unsigned long long* stats = nullptr;  // [candidates, iterations entered, message passes, converged]
+  unsigned long long* clock = nullptr;  // timed launches: [wave cycles, wave wall ticks, max wave cycles, waves]
   int slot0 = 0;           // batch index of slot 0 (records carry slot0 + local slot)
   int grid_waves = 4;      // k_bp persistent grid: resident waves per SIMD (clamped to 4)
   // mode 0, nullable: slots whose order of equal scores k_select deferred (warn bit 3) get it

@@ -381,6 +381,13 @@ int ft8_get_timing(ft8_ctx* ctx, double* ms, int64_t* launches, int reset);
 /* BP work counters, accumulated while timing is enabled: out4 = {candidates decoded, BP
  * iterations entered, message-passing sweeps executed, candidates converged}; synchronises. */
 int ft8_get_counters(ft8_ctx* ctx, int64_t* out4, int reset);
+/* k_bp's own clock, accumulated over launches made while timing is enabled (each persistent wave
+ * reads the shader-clock and the constant-rate wall-clock counters when it starts and when it
+ * retires): out5 = {sum of wave lifetimes in shader cycles, the same in wall-clock ticks, the
+ * longest wave lifetime in cycles, waves, wall-clock rate in kHz}.  Cycles per launch do not depend
+ * on the box's clock; cycles / wall time is the clock k_bp ran at.  Synchronises.  (No reference
+ * counterpart: measurement of ldpc_decoder.py:54-113's replacement.) */
+int ft8_get_bp_clock(ft8_ctx* ctx, int64_t* out5, int reset);
 
 #ifdef __cplusplus
 }
