@@ -36,6 +36,9 @@ Prints ONE JSON line on rank 0.  Besides the contract fields it carries:
   gather        (N > 1 or --gather) the last timed step's decode exchange: backend, rows and bytes per rank
   gather_n1     (N = 1) steps with vs without the N > 1 exchange (device pack + RCCL all-gather over a
                 world-size-1 group), interleaved blocks: its cost per step
+  sensitivity   the reference's own sensitivity harness (test_ft8_standard.py:43-123, the source of its
+                only published number) on the GPU: per sample rate the minimum
+                full-band SNR for >= 50 % decodes, next to the xlsx table, with an oracle-checked sample (N=1)
   reference_measured  the reference's own single-thread figure, for context
 """
 import argparse
@@ -220,7 +223,35 @@ def bp_parity(llr, x, plain, res, iters, n_sample):
             "oracle_s": time.perf_counter() - t0, "oracle": "oracle/ft8_oracle.c (bp_decode, ldpc_decoder.py:54-113)"}
 
 
-def bp_stress(ctx, dev, n=100000, iters=50, reps=3, sigma=0.85, n_sample=2000):
+def _oracle_bp_chunk(args):
+    from oracle import oracle as O
+    xs, iters = args
+    for v in xs:
+        O.bp_decode(v, iters)
+    return len(xs)
+
+
+def bp_cpu_baseline(xn, iters, procs, n_total):
+    """The oracle's bp_decode (oracle/ft8_oracle.c, pinned to ldpc_decoder.py:54-113) on the given
+    normalised LLR vectors, `procs` threads (ctypes releases the GIL), extrapolated to the GPU
+    launch's n_total vectors ("time 1 000 candidates and extrapolate")."""
+    from concurrent.futures import ThreadPoolExecutor
+    from oracle import oracle as O
+    O.lib()
+    n = xn.shape[0]
+    chunks = [(xn[i::procs], iters) for i in range(procs)]
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(procs) as ex:
+        done = sum(ex.map(_oracle_bp_chunk, chunks))
+    dt = time.perf_counter() - t0
+    return {"value": done / dt, "unit": "candidates/s", "cores": procs, "kind": "port",
+            "sample": f"{done} of the launch's normalised LLR vectors x {iters} BP iterations through "
+                      f"oracle/ft8_oracle.c bp_decode on {procs} threads, {dt:.2f} s wall",
+            "extrapolated_s_per_launch": n_total / (done / dt),
+            "extrapolation": f"linear in vectors: {n_total} vectors / the sample's rate"}
+
+
+def bp_stress(ctx, dev, n=100000, iters=50, reps=3, sigma=0.85, n_sample=2000, procs=1, n_cpu=2000):
     """BASELINE config 4 (first pass): n LLR vectors from codewords of random payloads,
     (2b-1) + sigma N(0,1), ftx_normalize_logl on the device, then ft8_bp with `iters` iterations.
     Returns candidates/s and the k_bp roofline for this launch shape."""
@@ -256,6 +287,7 @@ def bp_stress(ctx, dev, n=100000, iters=50, reps=3, sigma=0.85, n_sample=2000):
     ctx.check(L.ft8_bp(ctx.handle, _lib.ptr(x), n, iters, _lib.ptr(plain), _lib.ptr(res), st), "ft8_bp")
     torch.cuda.synchronize()
     parity = bp_parity(llr, x, plain, res, iters, n_sample)
+    cpu = bp_cpu_baseline(x[:n_cpu].cpu().numpy(), iters, procs, n) if n_cpu > 0 else None
     return {"workload": f"BASELINE config 4 first pass: {n} LLR vectors (codewords of random payloads, "
                         f"(2b-1)+{sigma}*N(0,1), normalised), {iters} BP iterations",
             "candidates_per_s": n * reps / dt, "ms_per_launch": bp_ms, "timing": "wall clock over back-to-back launches",
@@ -263,7 +295,7 @@ def bp_stress(ctx, dev, n=100000, iters=50, reps=3, sigma=0.85, n_sample=2000):
             "sweeps_per_launch": cn["passes"] / reps,
             "roofline": {"kernel": "k_bp", "bound": "fp64-valu", "achieved": tf, "peak": FP64_VECTOR_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": tf / FP64_VECTOR_PEAK_TFLOPS},
-            "parity": parity}
+            "parity": parity, "cpu_baseline": cpu}
 
 
 SUB_SEED0 = 200000
@@ -280,6 +312,7 @@ def subtract_oracle_worker(args):
     seed, signals, iters = args
     x, _ = synth.make_slots(1, signals, fs=12000, snr_db=(-24.0, -10.0), seeds=[seed], device="cpu")
     xs = x[0].numpy()
+    t0 = time.perf_counter()
     plan = make_plan(xs.shape[0], 12000)
     d1 = OS.decode_topk(xs, 12000, 300, 2, iters)
     recs = np.zeros(len(d1), dtype=[("payload", "u1", 10), ("ok", "u1"), ("abs_time", "<i4"), ("abs_freq", "<i4")])
@@ -289,9 +322,10 @@ def subtract_oracle_worker(args):
     res = OS.residual(xs, ofit, plan.nperseg, 12000).astype(np.float32)
     p1 = {pay for pay, _, _ in d1}
     new = {pay for pay, _, _ in OS.decode_topk(res, 12000, 300, 2, iters)} - p1
+    t_dec = time.perf_counter() - t0
     from oracle import oracle as O
     n_pass = int((O.score_grid(O.waterfall(xs, 12000, 2, 2), 2, 2) >= 2).sum())  # k_topkc's input size
-    return xs, sorted(p.hex() for p in p1), sorted(p.hex() for p in new), sum(f is not None for f in ofit), n_pass
+    return xs, sorted(p.hex() for p in p1), sorted(p.hex() for p in new), sum(f is not None for f in ofit), n_pass, t_dec
 
 
 def subtract_oracle(n, procs, signals=50, iters=50):
@@ -301,11 +335,18 @@ def subtract_oracle(n, procs, signals=50, iters=50):
     import numpy as np
     ctx = mp.get_context("fork")
     t0 = time.perf_counter()
-    with ctx.Pool(min(procs, n), initializer=_worker_init) as pool:
+    cores = min(procs, n)
+    with ctx.Pool(cores, initializer=_worker_init) as pool:
         out = pool.map(subtract_oracle_worker, [(SUB_SEED0 + b, signals, iters) for b in range(n)], chunksize=1)
+    t_dec = sum(o[5] for o in out)
     return (np.stack([o[0] for o in out]), [(o[1], o[2]) for o in out],
             {"fits": sum(o[3] for o in out), "oracle_wall_s": time.perf_counter() - t0,
-             "passing_scores_per_slot": float(np.mean([o[4] for o in out]))})
+             "passing_scores_per_slot": float(np.mean([o[4] for o in out])),
+             "cpu_baseline": {"value": n / t_dec * cores, "unit": "slots/s", "cores": cores, "kind": "port",
+                              "sample": f"{n} slots of this leg through oracle/subtract.py (both passes: top-k decode, "
+                                        f"fits, residual, top-k decode; {iters} BP iterations), one slot per process, "
+                                        f"{t_dec / n:.2f} s per slot (decode only, synthesis excluded)",
+                              "candidates_per_s": 2 * 300 * n / t_dec * cores}})
 
 
 def subtract_redecode(dev, n_slots=334, signals=50, iters=50, reps=3, oracle_sample=None):
@@ -352,6 +393,7 @@ def subtract_redecode(dev, n_slots=334, signals=50, iters=50, reps=3, oracle_sam
                   "oracle": "oracle/subtract.py (CPU float64 restatement of the build-defined second pass; the "
                             "reference has no second pass, so pass 2 is pinned to the restatement, not the reference)",
                   "from": "the first slots of this leg's batch, synthesised on the CPU and uploaded (same bytes)"}
+    cpu = oracle_sample[2].get("cpu_baseline") if oracle_sample is not None else None
     ctx = dec.ctx
     torch.cuda.synchronize()
     ctx.set_timing(True)
@@ -412,6 +454,7 @@ def subtract_redecode(dev, n_slots=334, signals=50, iters=50, reps=3, oracle_sam
             "true_decodes_per_slot_pass1": true1 / n_slots, "true_decodes_per_slot_pass2": true2 / n_slots,
             "false_decodes": int(false),
             "parity": parity,
+            "cpu_baseline": cpu,
             "rooflines": rl,
             "stages_ms": {k: v[0] / reps for k, v in tm.items() if v[1] > 0},
             "data": "synthetic (ft8_demodulator_amd.synth, seeds 200000..); the reference has no second pass: "
@@ -580,6 +623,120 @@ def drift_32k(dev, n_sig=16, reps=3):
             "stft_method": {0: "stockham", 1: "packed3840", 2: "chirp-z", 3: "direct DFT"}.get(method, method),
             "ms_per_signal": dt / n_sig * 1e3, "signals_per_s": n_sig / dt, "full_fits": int(ok.sum()),
             "median_abs_rate_err_hz_per_s": float(np.median(np.abs(est[ok] - true[ok]))) if ok.any() else None}
+
+
+# the reference's only published result, the minimum SNR (full band, B = fs/2)
+# for >= 50 % decodes, snr_vs_freq_analysis.xlsx sheet1 rows 3-14, keyed by sample rate fs = 2 B
+XLSX_MIN_SNR_DB = {2000: -9, 3000: -11, 4000: -12, 5000: -13, 6000: -13, 7000: -14, 8000: -14, 9000: -16,
+                   10000: -16, 11000: -17, 12000: -17, 13000: -17}
+SENSITIVITY_RATES = sorted(set(range(2000, 10001, 500)) | {11000, 12000, 13000})
+
+
+def _oracle_decode_payloads(args):
+    from oracle import oracle as O
+    x, fs = args
+    return [bytes(r[0]).hex() for r in O.decode_ft8_message(x, fs, 2, 2, 20, 1, 20)]
+
+
+def sensitivity(dev, rates=None, snr_lo=-24.0, snr_hi=-5.0, step=0.2, rounds=20, seed=31337, chunk=2048,
+                oracle_per_rate=2, procs=1):
+    """The reference's sensitivity harness on the GPU (test_ft8_standard.py:43-123): at each sample
+    rate, for SNR from snr_lo to snr_hi in `step` dB, `rounds` independent test_step's -- a random
+    payload (np.random.randint(0, 256, 10)) -> the reference-timing GFSK waveform with f0 = fc = 0
+    (ft8_synthesize, FT8_TX_REFERENCE: modulator.py:27-90, float64) -> white noise at the SNR of the
+    full band (signal power = mean(wave^2), :51-54) -> decode_ft8_message(bins_per_tone =
+    steps_per_symbol = 2, max_candidates 20, min_score 1, 20 iterations) -> success if anything
+    decodes.  The minimum SNR is the first (lowest) SNR whose success ratio reaches 0.5 (:99-107; the
+    reference stops a point early once 11 of 20 failed, which cannot change that test).  All points
+    and rounds of a rate are one float64 batch on the GPU.  A sample of slots per rate (the two
+    rounds at the rate's threshold SNR) is decoded again by the oracle (C + scipy) from the same
+    float64 bytes: `parity`."""
+    import numpy as np
+    import torch
+    from concurrent.futures import ThreadPoolExecutor
+    from ft8_demodulator_amd import SlotDecoder, _lib
+    from ft8_demodulator_amd import ft8_generator as G
+    rates = rates or SENSITIVITY_RATES
+    snrs = np.round(np.arange(snr_lo, snr_hi + step / 2, step), 6)
+    n_pts = len(snrs)
+    gen = torch.Generator(device=dev)
+    rng = np.random.default_rng(seed)
+    table, samples, t_dec, n_dec_slots = [], [], 0.0, 0
+    for fs in rates:
+        nsps = int(0.16 * fs)
+        n = 79 * nsps
+        n_slots = n_pts * rounds
+        snr_of = np.repeat(snrs, rounds)        # slot i: SNR point i // rounds
+        pay = rng.integers(0, 256, size=(n_slots, 10), dtype=np.uint8)
+        _, _, tones = G.encode_batch(pay, 10, device=dev)
+        dec = SlotDecoder(fs, 2, 2, max_candidates=20, min_score=1, max_iterations=20, device=dev)
+        success = np.zeros(n_slots, dtype=bool)
+        keep = {}
+        for c0 in range(0, n_slots, chunk):
+            c1 = min(n_slots, c0 + chunk)
+            sig = np.zeros(c1 - c0, dtype=_lib.TX_SIGNAL_DTYPE)
+            sig["amplitude"], sig["slot"] = 1.0, np.arange(c1 - c0)
+            clean = G.synthesize(tones[c0:c1], sig, c1 - c0, n, fs, _lib.FT8_TX_REFERENCE, dtype=torch.float64,
+                                 device=dev)
+            gen.manual_seed(seed * 1000003 + fs * 1009 + c0)
+            p_sig = (clean * clean).mean(dim=1)
+            snr_t = torch.as_tensor(snr_of[c0:c1], dtype=torch.float64, device=dev)
+            x = clean + torch.sqrt(p_sig / 10.0 ** (snr_t / 10.0))[:, None] * torch.randn(
+                clean.shape, dtype=torch.float64, device=dev, generator=gen)
+            del clean
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            _, counts = dec.run(x, _lib.FT8_F64)
+            torch.cuda.synchronize()
+            t_dec += time.perf_counter() - t0
+            n_dec_slots += c1 - c0
+            success[c0:c1] = counts.cpu().numpy() > 0
+            # the oracle sample is picked once the threshold is known: the chunk stays on the device
+            # until then (a rate's batch is a few GB at most)
+            keep[c0] = x
+        ok = success.reshape(n_pts, rounds).sum(axis=1)
+        hit = np.nonzero(ok >= rounds * 0.5)[0]
+        thr = float(snrs[hit[0]]) if hit.size else None
+        # 50 % crossing by linear interpolation of the success ratio (a finer figure than the grid's)
+        ratio = ok / rounds
+        cross = None
+        if hit.size and hit[0] > 0:
+            j = hit[0]
+            r0, r1 = ratio[j - 1], ratio[j]
+            cross = float(snrs[j - 1] + (0.5 - r0) / (r1 - r0) * (snrs[j] - snrs[j - 1])) if r1 > r0 else float(snrs[j])
+        row = {"fs": fs, "bandwidth_hz": fs / 2, "min_snr_db": thr, "crossing_50pct_db": cross,
+               "xlsx_min_snr_db": XLSX_MIN_SNR_DB.get(fs),
+               "success_per_point": {f"{s_:.1f}": int(k_) for s_, k_ in zip(snrs, ok) if 0 < k_ < rounds}}
+        table.append(row)
+        # oracle sample: the first `oracle_per_rate` rounds at the threshold point (or the top point)
+        jp = hit[0] if hit.size else n_pts - 1
+        for r_ in range(min(oracle_per_rate, rounds)):
+            i = jp * rounds + r_
+            c0 = (i // chunk) * chunk
+            x_host = keep[c0][i - c0].cpu().numpy()
+            gpu_pay = [bytes(p_).hex() for p_ in dec.records(keep[c0][i - c0:i - c0 + 1], _lib.FT8_F64)[0]["payload"]]
+            samples.append((fs, float(snr_of[i]), x_host, gpu_pay))
+        del keep
+        torch.cuda.empty_cache()
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(max(1, procs)) as ex:   # ctypes and scipy release the GIL
+        cpu = list(ex.map(_oracle_decode_payloads, [(x_, fs_) for fs_, _s, x_, _g in samples]))
+    t_cpu = time.perf_counter() - t0
+    mism = [{"fs": fs_, "snr_db": s_, "gpu": g_, "oracle": c_} for (fs_, s_, _x, g_), c_ in zip(samples, cpu) if g_ != c_]
+    return {"method": "test_ft8_standard.py:43-123 on the GPU: f0 = fc = 0, bins_per_tone = steps_per_symbol = 2, "
+                      "K = 20, min_score 1, 20 iterations, float64 input; SNR over the full band (B = fs / 2); "
+                      f"{snr_lo} .. {snr_hi} dB in {step} dB steps, {rounds} rounds per point; min_snr_db = the "
+                      "first point with >= 50 % decodes (the reference's rule), crossing_50pct_db = the linear "
+                      "interpolation of the success ratio at 0.5",
+            "rounds": rounds, "slots": n_dec_slots, "decode_slots_per_s": n_dec_slots / t_dec if t_dec else None,
+            "table": table,
+            "parity": {"slots": len(samples), "equal": len(samples) - len(mism), "mismatches": mism[:8],
+                       "what": "payload lists, GPU vs oracle on the same float64 bytes (the rounds at each "
+                               "rate's threshold SNR)", "oracle_threads": procs, "oracle_wall_s": t_cpu},
+            "cpu_baseline": {"value": len(samples) / t_cpu if t_cpu else None, "unit": "slots/s",
+                             "cores": procs, "kind": "port",
+                             "sample": f"the {len(samples)} parity slots above, oracle/ft8_oracle.c + scipy, "
+                                       f"{procs} threads"}}
 
 
 def drift_correct(dev, n_sig=256, reps=5):
@@ -866,6 +1023,8 @@ def main():
                     help="slots of the subtract leg checked against oracle/subtract.py (0: none)")
     ap.add_argument("--no-drift", action="store_true", help="skip the frequency-drift correction leg")
     ap.add_argument("--no-geometries", action="store_true", help="skip the 20 kHz / bpt=10 geometry legs")
+    ap.add_argument("--no-sensitivity", action="store_true",
+                    help="skip the reference's sensitivity harness (test_ft8_standard.py) on the GPU")
     ap.add_argument("--gather", action="store_true",
                     help="N = 1: every timed step also packs its decodes and all-gathers them over a world-size-1 "
                          "RCCL group (the per-step exchange of the N > 1 path)")
@@ -1110,7 +1269,7 @@ def main():
 
     stress = None
     if world == 1 and not args.no_bp_stress:
-        stress = bp_stress(ctx, dev)
+        stress = bp_stress(ctx, dev, procs=host_cores()[0])
     stream = None
     if world == 1 and not args.no_h2d:
         stream = h2d_stream(x, max(3, min(args.steps, 10)), kw)
@@ -1123,6 +1282,9 @@ def main():
     geoms = None
     if world == 1 and not args.no_geometries:
         geoms = geometry_legs(dev)
+    sens = None
+    if world == 1 and not args.no_sensitivity:
+        sens = sensitivity(dev, procs=host_cores()[0])
     sub = None
     if world == 1 and not args.no_subtract:
         sub = subtract_redecode(dev, oracle_sample=sub_oracle)
@@ -1207,6 +1369,7 @@ def main():
         "subtract_redecode": sub,
         "drift_correct": drift,
         "geometries": geoms,
+        "sensitivity": sens,
         "cpu_baseline": cpu,
         "parity": parity,
         "reference_measured": REFERENCE_MEASURED,

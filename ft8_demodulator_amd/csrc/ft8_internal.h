@@ -35,8 +35,15 @@ __device__ __forceinline__ void race_prologue() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __syncthreads();
   const uint32_t nw = (nt + kWave - 1) / kWave;
-  if (nw > 1 && t / kWave == blockIdx.x % nw)
+  // the test must be wave-uniform in an SGPR: s_sleep is a scalar instruction that the EXEC mask
+  // does not gate, so under a per-lane condition (an exec-masked block the compiler does not branch
+  // around) every wave slept and none was late -- the positive control caught it
+  const uint32_t w = __builtin_amdgcn_readfirstlane(t / kWave);
+  if (nw > 1 && w == blockIdx.x % nw)
     for (int i = 0; i < 8; ++i) __builtin_amdgcn_s_sleep(127);
+  // a compiler barrier: s_sleep carries no memory semantics, so the kernel's first LDS accesses
+  // must not be scheduled above it
+  asm volatile("" ::: "memory");
 }
 #define FT8_RACE_PROLOGUE() ::ft8::race_prologue()
 #else

@@ -462,10 +462,10 @@ struct PkArgs {
   const f2* post;  // W_2P^k, k in [0, P]
 };
 
-// one Stockham stage (not the first): butterfly j = t + 256 b of nbf = P / R, Ns = NS
-template <int P, int NS, int R>
+// one Stockham stage (not the first): butterfly j = t + TH b of nbf = P / R, Ns = NS
+template <int TH, int P, int NS, int R>
 __device__ __forceinline__ void pk_stage(f2* buf, const f2* tw) {
-  constexpr int NBF = P / R, NB = (NBF + kThreads38 - 1) / kThreads38, TSTEP = P / (NS * R);
+  constexpr int NBF = P / R, NB = (NBF + TH - 1) / TH, TSTEP = P / (NS * R);
   // every index step is a multiple of 16, so pidx(x + 16 m) = pidx(x) + 17 m: one address per
   // butterfly and immediates (as k_stft3840p)
   static_assert(NBF % 16 == 0 && NS % 16 == 0, "linear padded index steps");
@@ -474,7 +474,7 @@ __device__ __forceinline__ void pk_stage(f2* buf, const f2* tw) {
   f2 v[NB][R];
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
-    const int j = t + kThreads38 * b;
+    const int j = t + TH * b;
     if (j < NBF) {
       const int base = pidx(j);
 #pragma unroll
@@ -484,7 +484,7 @@ __device__ __forceinline__ void pk_stage(f2* buf, const f2* tw) {
   __syncthreads();  // every read of the image is done: write in place
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
-    const int j = t + kThreads38 * b;
+    const int j = t + TH * b;
     if (j < NBF) {
       const int k = j % NS;
       if (k != 0) {
@@ -510,14 +510,16 @@ __device__ __forceinline__ void pk_stage(f2* buf, const f2* tw) {
   __syncthreads();
 }
 
-template <int P, int NS, int R, int... Rest>
+template <int TH, int P, int NS, int R, int... Rest>
 __device__ __forceinline__ void pk_stages(f2* buf, const f2* tw) {
-  pk_stage<P, NS, R>(buf, tw);
-  if constexpr (sizeof...(Rest) > 0) pk_stages<P, NS * R, Rest...>(buf, tw);
+  pk_stage<TH, P, NS, R>(buf, tw);
+  if constexpr (sizeof...(Rest) > 0) pk_stages<TH, P, NS * R, Rest...>(buf, tw);
 }
 
-template <typename InT, int P, int... Rs>
-__global__ __launch_bounds__(kThreads38) void k_stft_pk(PkArgs a) {
+// TH threads per frame: 256, or 512 for the 9 600-point plan, whose 82 KB image allows only two
+// workgroups per CU (8 resident waves at 256 threads: the barriers between stages left the SIMDs idle)
+template <typename InT, int TH, int P, int... Rs>
+__global__ __launch_bounds__(TH) void k_stft_pk(PkArgs a) {
   FT8_RACE_PROLOGUE();
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_pk[];
   f2* buf = reinterpret_cast<f2*>(smem_pk);
@@ -531,10 +533,10 @@ __global__ __launch_bounds__(kThreads38) void k_stft_pk(PkArgs a) {
   // stage 1: radix 16, Ns = 1, over the frame's nonzero half: inputs z[j + r P / 16], r < 8, with
   // z[n] = (w[2n] x[2n], w[2n+1] x[2n+1]) (zero past nperseg) -> buf[16 j + k]
   {
-    constexpr int NBF = P / 16, NB = (NBF + kThreads38 - 1) / kThreads38;
+    constexpr int NBF = P / 16, NB = (NBF + TH - 1) / TH;
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
-      const int j = t + kThreads38 * b;
+      const int j = t + TH * b;
       if (j < NBF) {
         f2 z[8], y[16];
 #pragma unroll
@@ -553,7 +555,7 @@ __global__ __launch_bounds__(kThreads38) void k_stft_pk(PkArgs a) {
     }
     __syncthreads();
   }
-  pk_stages<P, 16, Rs...>(buf, a.tw);
+  pk_stages<TH, P, 16, Rs...>(buf, a.tw);
   // epilogue: X[k] = (s - i W_2P^k d) / 2, s = Z[k] + conj Z[P-k], d = Z[k] - conj Z[P-k]
   constexpr float kDb = 3.0102999566398119521f;  // 10 log10(v) = (10 log10 2) log2(v), v >= 1e-12
   const float qscale = 0.25f * a.scale;          // |2 X|^2 / 4 / (sum w)^2
@@ -561,7 +563,7 @@ __global__ __launch_bounds__(kThreads38) void k_stft_pk(PkArgs a) {
   if (a.f_lo == 0 && a.nf_out == P) {
     // every f >= 0 bin kept: bins k and P - k share s and d (k_stft3840p's full-band epilogue):
     // one pair of LDS reads, one post-twiddle and one packed power for both
-    for (int k = t; k <= P / 2; k += kThreads38) {
+    for (int k = t; k <= P / 2; k += TH) {
       const f2 A = lds_ld(&buf[pidx(k)]);
       const f2 B = lds_ld(&buf[pidx(k == 0 ? 0 : P - k)]);
       const f2 sm = add_cj(A, B), df = sub_cj(A, B);
@@ -573,7 +575,7 @@ __global__ __launch_bounds__(kThreads38) void k_stft_pk(PkArgs a) {
     }
     return;
   }
-  for (int i = t; i < a.nf_out; i += kThreads38) {
+  for (int i = t; i < a.nf_out; i += TH) {
     const int k = a.f_lo + i;
     const int kk = (k <= P) ? k : 2 * P - k;  // real signal: X[N-k] = conj X[k]
     const f2 A = lds_ld(&buf[pidx(kk == P ? 0 : kk)]);
@@ -624,6 +626,7 @@ hipError_t launch_stft3840(const StftLaunch& L, hipStream_t s) {
 struct PkPlan {
   int P, n, r[4];
 };
+constexpr int kPk9600Threads = 512;
 constexpr PkPlan kPkPlans[] = {{3200, 4, {16, 8, 5, 5}}, {9600, 4, {16, 8, 15, 5}}, {960, 3, {16, 4, 15}}};
 
 static int pk_plan_of(const StftLaunch& L) {
@@ -667,14 +670,16 @@ hipError_t launch_stftpk(const StftLaunch& L, hipStream_t s) {
       hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(kern, grid, dim3(kThreads38), lds, s, a);
+    hipLaunchKernelGGL(kern, grid, dim3(q == 1 ? kPk9600Threads : kThreads38), lds, s, a);
     return hipGetLastError();
   };
   const bool i16 = L.dtype == FT8_I16;
   switch (q) {
-    case 0: return i16 ? go(k_stft_pk<int16_t, 3200, 8, 5, 5>) : go(k_stft_pk<float, 3200, 8, 5, 5>);
-    case 1: return i16 ? go(k_stft_pk<int16_t, 9600, 8, 15, 5>) : go(k_stft_pk<float, 9600, 8, 15, 5>);
-    default: return i16 ? go(k_stft_pk<int16_t, 960, 4, 15>) : go(k_stft_pk<float, 960, 4, 15>);
+    case 0: return i16 ? go(k_stft_pk<int16_t, kThreads38, 3200, 8, 5, 5>) : go(k_stft_pk<float, kThreads38, 3200, 8, 5, 5>);
+    case 1:
+      return i16 ? go(k_stft_pk<int16_t, kPk9600Threads, 9600, 8, 15, 5>)
+                 : go(k_stft_pk<float, kPk9600Threads, 9600, 8, 15, 5>);
+    default: return i16 ? go(k_stft_pk<int16_t, kThreads38, 960, 4, 15>) : go(k_stft_pk<float, kThreads38, 960, 4, 15>);
   }
 }
 

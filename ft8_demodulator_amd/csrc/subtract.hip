@@ -50,14 +50,6 @@ __device__ __forceinline__ float ld_sample<int16_t>(const int16_t* x, int64_t i)
 }
 
 __device__ __forceinline__ float ramp_f(int n, int L, int nsps) { return tx::gfsk_ramp<float>(n, L, nsps, 0); }
-// the amplitude ramp at sample n of symbol k: 1 except in the first and last symbols (the ramps are
-// nsps / 8 long).  The ramp's cos and division are a call there: inlined, the compiler evaluated
-// them for every sample of every symbol (~60 of the per-sample loop's ~120 VALU instructions)
-__device__ __noinline__ float ramp_edge(int n, int L, int nsps) { return ramp_f(n, L, nsps); }
-__device__ __forceinline__ float ramp_at(int k, int n, int L, int nsps) {
-  return (k == 0 || k == tx::kSymbols - 1) ? ramp_edge(n, L, nsps) : 1.0f;
-}
-
 // k_sub_list: one wave per slot lists the records worth a fit -- ok, and the first record of the
 // slot carrying its payload (a crowded top-k slot decodes ~40 records for ~21 distinct messages) --
 // in record order, and marks every record inactive (k_sub_est then activates the ones it fits), so
@@ -97,7 +89,12 @@ __global__ __launch_bounds__(kWave) void k_sub_list(SubLaunch a) {
 template <typename InT, bool REST>
 __global__ __launch_bounds__(kSubThreads) void k_sub_est(SubLaunch a) {
   FT8_RACE_PROLOGUE();
-  // dynamic LDS: the decimated baseband z (phases 2-3), then the float pulse table (phase 4)
+  // dynamic LDS: the decimated baseband z (phases 2-3), then the float pulse table (phase 4).  z is
+  // stored in rows of Q + 1 (one pad): row r + 1 holds z[1 + r Q .. 1 + (r + 1) Q), r = -1 .. 81,
+  // so symbol k's window starts a row (z_at below) and the lanes' reads (one symbol per lane) are
+  // 2 (Q + 1) dwords apart -- distinct banks for even Q.  Unpadded, the lanes of a ds_read_b64
+  // were 2 Q dwords apart: at Q = 32 one bank for all 32 lanes of a group (32-way conflicts; 169 M
+  // conflict cycles per 334-slot launch, r4_v30_sub_pmc.json)
   extern __shared__ float4 s_dyn[];
   float2* s_z = reinterpret_cast<float2*>(s_dyn);
   float4* s_D = s_dyn;  // phase 4: the pulse table's symbol-relative differences (see k_sub_apply)
@@ -147,6 +144,8 @@ __global__ __launch_bounds__(kSubThreads) void k_sub_est(SubLaunch a) {
   const int Mt = (Q + 2 * (nsps / a.hop) - 1) / (2 * (nsps / a.hop));  // ceil((hop / 2) / D)
   const int Mg = Mt + 1;
   const int Mz = tx::kSymbols * Q + 2 * Mg;
+  // z[m] -> its padded position (m >= 0; Mg - Mt = 1 is the first window's start)
+  auto z_at = [Q](int m) { const int u = m - 1 + Q; return u + (int)((unsigned)u / (unsigned)Q); };
   const double fs = (double)a.fs;
   const int64_t s0 = (int64_t)(a.t_lo + r.abs_time) * a.hop;
   const double ftone = (double)(a.f_lo + r.abs_freq) * fs / (double)a.nfft;
@@ -209,7 +208,7 @@ __global__ __launch_bounds__(kSubThreads) void k_sub_est(SubLaunch a) {
       }
 #pragma unroll
       for (int q = 0; q < 2; ++q)
-        if (m[q] < Mz && j0 + q < kZ) s_z[m[q]] = acc[q];
+        if (m[q] < Mz && j0 + q < kZ) s_z[z_at(m[q])] = acc[q];
     }
   }
   __syncthreads();
@@ -241,7 +240,7 @@ __global__ __launch_bounds__(kSubThreads) void k_sub_est(SubLaunch a) {
       for (int d = 0; d < kMaxT; ++d) msum[d] = 0.f;
       for (int k = lane; k < tx::kSymbols; k += kWave) {
         const float2 w = s_st[f * 8 + s_tones[k]];
-        const float2* zp = s_z + Mg - Mt + k * Q;
+        const float2* zp = s_z + (k + 1) * (Q + 1);  // = z_at(Mg - Mt + k Q): z[.. + j] at zp[j + j / Q]
         float2 acc = make_float2(0.f, 0.f), wq = make_float2(1.f, 0.f);
         for (int q = 0; q < Q; ++q) {
           const float2 z = zp[q];
@@ -254,7 +253,8 @@ __global__ __launch_bounds__(kSubThreads) void k_sub_est(SubLaunch a) {
           if (d < nT) {
             msum[d] += acc.x * acc.x + acc.y * acc.y;
             if (d + 1 < nT) {
-              const float2 zo = zp[d], zn = zp[d + Q];
+              const int dq = d + (d >= Q ? 1 : 0);  // d < 2 Q
+              const float2 zo = zp[dq], zn = zp[dq + Q + 1];
               const float tx_ = acc.x - zo.x + (zn.x * wq.x - zn.y * wq.y);
               const float ty_ = acc.y - zo.y + (zn.x * wq.y + zn.y * wq.x);
               acc = make_float2(tx_ * w.x + ty_ * w.y, ty_ * w.x - tx_ * w.y);
@@ -400,44 +400,59 @@ __global__ __launch_bounds__(kSubThreads) void k_sub_est(SubLaunch a) {
   }  // records
 }
 
+constexpr int kApThreads = 512;
 constexpr int kApPer = 16;
-constexpr int kApTile = kSubThreads * kApPer;
+constexpr int kApTile = kApThreads * kApPer;   // samples per workgroup
 constexpr int kApFits = 4;                     // fits staged in LDS per batch
 constexpr int kApList = 1024;                  // overlapping fits listed per pass over the records
 
-// One workgroup per (slot, tile of 4096 samples).  Wave 0 lists the fits that overlap the tile, in
-// record order; their parameters (tones as floats, amplitudes, symbol phases, start, f0) are staged
-// kApFits at a time; every thread then adds each staged fit's waveform to its 16 samples.  A
-// thread's samples are 256 apart, so its symbol index k and in-symbol offset i advance by one
-// addition each (one floor division per fit and thread instead of one per sample).
+// One workgroup per (slot, tile of 8192 samples).  Wave 0 lists the fits that overlap the tile, in
+// record order; per batch of kApFits fits, everything one SYMBOL of a fit needs is staged once:
+// s_S1 = (E[k], E[k+1], E[k+2], phase0[k]) -- the extended tones whose pulses reach symbol k and
+// its start phase -- s_S2 = (A[k], A[k] - A[k-1]) and s_S3 = A[k+1] - A[k], the amplitude and its
+// slopes before and after the symbol centre (A clamped at the ends, as in the interpolation).  A
+// thread's 16 samples are 512 apart; per fit it finds its first sample's symbol k and offset i once
+// (one floor division), keeps symbol k's state in registers, and reloads it only when i wraps past
+// nsps (every ~4 samples at 12 kHz).  Per sample and fit that leaves the pulse-table read, the phase,
+// fract / sin / cos, the interpolated amplitude and one add -- round 4's form re-derived the symbol
+// state (6 LDS reads, clamps, selects and their addresses) for every sample.  The amplitude ramp
+// (first and last symbol only) is a table of nsps / 8 floats in LDS, the values tx_device.h's
+// gfsk_ramp computes (both ramps of the protocol timing are 0.5 (1 - cos(8 pi j / nsps))).
+// Every arithmetic step is the round-4 form's, in its order: the residual is bit-identical.
 template <typename InT>
-__global__ __launch_bounds__(kSubThreads) void k_sub_apply(SubLaunch a) {
+__global__ __launch_bounds__(kApThreads) void k_sub_apply(SubLaunch a) {
   FT8_RACE_PROLOGUE();
-  __shared__ float s_E[kApFits][tx::kExt];
-  __shared__ float2 s_A[kApFits][tx::kSymbols];
-  __shared__ float s_ph0[kApFits][tx::kSymbols + 1];
+  __shared__ float4 s_S1[kApFits][tx::kSymbols];
+  __shared__ float4 s_S2[kApFits][tx::kSymbols];
+  __shared__ float2 s_S3[kApFits][tx::kSymbols];
   __shared__ long long s_start[kApFits];
   __shared__ float s_f0r[kApFits];
   __shared__ short s_list[kApList];
   __shared__ int s_nlist;
   // the pulse table's three symbol-relative differences per in-symbol offset i, one float4 each:
-  // (P[i + 2 nsps] - P[2 nsps], P[i + nsps] - P[nsps], P[i] - P[0]) -- one ds_read_b128 and no
-  // subtractions per sample instead of six reads and three subtractions (same values: the
-  // subtractions of the pulse table the phase is built from)
+  // (P[i + 2 nsps] - P[2 nsps], P[i + nsps] - P[nsps], P[i] - P[0], t(i)) -- one ds_read_b128 and
+  // no subtractions per sample; then the ramp table [nsps / 8]
   extern __shared__ float4 s_D[];
   const int slot = blockIdx.y;
   const int64_t t0 = (int64_t)blockIdx.x * kApTile;
-  const int nsps = a.nsps, L = tx::kSymbols * nsps;
+  const int nsps = a.nsps, L = tx::kSymbols * nsps, nramp = nsps / 8;
+  float* s_R = reinterpret_cast<float*>(s_D + nsps);
   const float fsf = (float)a.fs, inv_nsps = 1.0f / (float)nsps, sr = 6.25f / fsf;
   const int cnt = min(a.counts[slot], a.cap);
   const SubEst* est = reinterpret_cast<const SubEst*>(a.est) + (int64_t)slot * a.cap;
+  // samples t0 + tid + 512 kk with kk < nv exist (16 except in a slot's last tile)
+  const int64_t rem = a.n_samples - (t0 + (int64_t)threadIdx.x);
+  const int nv = rem <= 0 ? 0 : (int)min<int64_t>(kApPer, (rem + kApThreads - 1) / kApThreads);
   float acc[kApPer];
 #pragma unroll
   for (int k = 0; k < kApPer; ++k) acc[k] = 0.f;
-  for (int i = threadIdx.x; i < nsps; i += kSubThreads) {
+  for (int i = threadIdx.x; i < nsps; i += kApThreads) {
     const float* P = a.Pf;
-    s_D[i] = make_float4(P[i + 2 * nsps] - P[2 * nsps], P[i + nsps] - P[nsps], P[i] - P[0], 0.0f);
+    // .w: the sample's position from the symbol centre in symbols, t(i) (the amplitude interpolation)
+    s_D[i] = make_float4(P[i + 2 * nsps] - P[2 * nsps], P[i + nsps] - P[nsps], P[i] - P[0],
+                         ((float)i + 0.5f) * inv_nsps - 0.5f);
   }
+  for (int i = threadIdx.x; i < nramp; i += kApThreads) s_R[i] = ramp_f(i, L, nsps);
   for (int j0 = 0; j0 < cnt; j0 += kApList) {
     __syncthreads();  // the previous list is consumed
     if (threadIdx.x < kWave) {
@@ -462,20 +477,14 @@ __global__ __launch_bounds__(kSubThreads) void k_sub_apply(SubLaunch a) {
     for (int b0 = 0; b0 < nl; b0 += kApFits) {
       const int nb = min(kApFits, nl - b0);
       __syncthreads();  // the previous batch is consumed
-      for (int q = threadIdx.x; q < nb * tx::kExt; q += kSubThreads) {
-        const int f = q / tx::kExt, kk = q - f * tx::kExt;
+      for (int q = threadIdx.x; q < nb * tx::kSymbols; q += kApThreads) {
+        const int f = q / tx::kSymbols, k = q - f * tx::kSymbols;
         const SubEst* e = est + j0 + s_list[b0 + f];
-        const int jj = kk - 1;
-        s_E[f][kk] = (float)e->tones[jj < 0 ? 0 : (jj > tx::kSymbols - 1 ? tx::kSymbols - 1 : jj)];
-      }
-      for (int q = threadIdx.x; q < nb * tx::kSymbols; q += kSubThreads) {
-        const int f = q / tx::kSymbols, kk = q - f * tx::kSymbols;
-        const SubEst* e = est + j0 + s_list[b0 + f];
-        s_A[f][kk] = make_float2(e->amp[kk][0], e->amp[kk][1]);
-      }
-      for (int q = threadIdx.x; q < nb * (tx::kSymbols + 1); q += kSubThreads) {
-        const int f = q / (tx::kSymbols + 1), kk = q - f * (tx::kSymbols + 1);
-        s_ph0[f][kk] = est[j0 + s_list[b0 + f]].phase0[kk];
+        const int km = k > 0 ? k - 1 : 0, kp = k < tx::kSymbols - 1 ? k + 1 : k;
+        s_S1[f][k] = make_float4((float)e->tones[km], (float)e->tones[k], (float)e->tones[kp], e->phase0[k]);
+        const float cx = e->amp[k][0], cy = e->amp[k][1];
+        s_S2[f][k] = make_float4(cx, cy, cx - e->amp[km][0], cy - e->amp[km][1]);
+        s_S3[f][k] = make_float2(e->amp[kp][0] - cx, e->amp[kp][1] - cy);
       }
       if (threadIdx.x < nb) {
         const SubEst* e = est + j0 + s_list[b0 + threadIdx.x];
@@ -486,31 +495,53 @@ __global__ __launch_bounds__(kSubThreads) void k_sub_apply(SubLaunch a) {
       for (int f = 0; f < nb; ++f) {
         const int64_t start = s_start[f];
         const float f0r = s_f0r[f];
-        const float* E = s_E[f];
         const int nr0 = (int)(t0 + threadIdx.x - start);  // |nr0| < 2^31: slots hold < 2^31 samples
         int k = nr0 >= 0 ? nr0 / nsps : -((-nr0 + nsps - 1) / nsps);  // floor
         int i = nr0 - k * nsps;
+        // symbol k's state (zeros outside the waveform: those samples are skipped)
+        float4 e4 = make_float4(0.f, 0.f, 0.f, 0.f), a4 = e4;
+        float2 r2 = make_float2(0.f, 0.f);
+        bool edge = false;  // symbol 0 or 78: the amplitude ramps
+        if ((unsigned)k < (unsigned)tx::kSymbols) {
+          e4 = s_S1[f][k];
+          a4 = s_S2[f][k];
+          r2 = s_S3[f][k];
+          edge = k == 0 || k == tx::kSymbols - 1;
+        }
 #pragma unroll
         for (int kk = 0; kk < kApPer; ++kk) {
-          const int64_t nabs = t0 + threadIdx.x + (int64_t)kk * kSubThreads;
-          if (k >= 0 && k < tx::kSymbols && nabs < a.n_samples) {
+          if ((unsigned)k < (unsigned)tx::kSymbols && kk < nv) {
             // the change of G over the symbol's first i samples (tx_device.h's pulse table)
             const float4 dd = s_D[i];
-            const float g = E[k] * dd.x + E[k + 1] * dd.y + E[k + 2] * dd.z;
-            const float cyc = s_ph0[f][k] + (float)i * f0r + sr * g;
+            const float g = e4.x * dd.x + e4.y * dd.y + e4.z * dd.z;
+            const float fi = (float)i;
+            const float cyc = e4.w + fi * f0r + sr * g;
             const float fr = __builtin_amdgcn_fractf(cyc);  // v_sin / v_cos take revolutions
             const float sn = __builtin_amdgcn_sinf(fr), cs = __builtin_amdgcn_cosf(fr);
-            const float t = ((float)i + 0.5f) * inv_nsps - 0.5f;  // position from the symbol centre
-            const float2 c = s_A[f][k];
-            const float2 o = t < 0.f ? s_A[f][k > 0 ? k - 1 : 0] : s_A[f][k < tx::kSymbols - 1 ? k + 1 : k];
-            const float2 A = t < 0.f ? make_float2(c.x + t * (c.x - o.x), c.y + t * (c.y - o.y))
-                                     : make_float2(c.x + t * (o.x - c.x), c.y + t * (o.y - c.y));
-            acc[kk] += ramp_at(k, k * nsps + i, L, nsps) * (A.x * cs - A.y * sn);
+            const float t = dd.w;  // position from the symbol centre
+            const float dx = t < 0.f ? a4.z : r2.x, dy = t < 0.f ? a4.w : r2.y;
+            const float Ax = a4.x + t * dx, Ay = a4.y + t * dy;
+            float v = Ax * cs - Ay * sn;
+            // the amplitude ramp: 1 except in the first nsps / 8 samples of symbol 0 and the last
+            // nsps / 8 of symbol 78 (the same float as 1 * v elsewhere)
+            if (edge) {
+              const int j = k == 0 ? i : nsps - 1 - i;
+              if (j < nramp) v = s_R[j] * v;
+            }
+            acc[kk] += v;
           }
-          i += kSubThreads;
-          while (i >= nsps) {
-            i -= nsps;
-            ++k;
+          i += kApThreads;
+          if (i >= nsps) {
+            do {
+              i -= nsps;
+              ++k;
+            } while (i >= nsps);
+            if ((unsigned)k < (unsigned)tx::kSymbols) {
+              e4 = s_S1[f][k];
+              a4 = s_S2[f][k];
+              r2 = s_S3[f][k];
+              edge = k == 0 || k == tx::kSymbols - 1;
+            }
           }
         }
       }
@@ -520,7 +551,7 @@ __global__ __launch_bounds__(kSubThreads) void k_sub_apply(SubLaunch a) {
   float* out = a.residual + (int64_t)slot * a.slot_stride;
 #pragma unroll
   for (int kk = 0; kk < kApPer; ++kk) {
-    const int64_t nabs = t0 + threadIdx.x + (int64_t)kk * kSubThreads;
+    const int64_t nabs = t0 + threadIdx.x + (int64_t)kk * kApThreads;
     if (nabs < a.n_samples) out[nabs] = ld_sample<InT>(x, nabs) - acc[kk];
   }
 }
@@ -583,7 +614,7 @@ hipError_t launch_sub_est(const SubLaunch& a, hipStream_t s) {
     // the rest launch: 8 workgroups per slot that exit at once unless the slot holds more than
     // kSubRecStride fits
     const unsigned grid_rest = (unsigned)(((a.n_slots + 7) / 8) * 8 * (int64_t)kSubRestStride);
-    const size_t mz = (size_t)tx::kSymbols * a.Q + 2 * (a.Q / (2 * (a.nsps / a.hop)) + 2);
+    const size_t mz = (size_t)(tx::kSymbols + 4) * (a.Q + 1);  // padded z rows -1 .. 81 (k_sub_est)
     const size_t lds = std::max(mz * sizeof(float2), (size_t)a.nsps * sizeof(float4));
     hipError_t e = hipSuccess;
     if (a.dtype == FT8_I16) {
@@ -609,14 +640,14 @@ hipError_t launch_sub_est(const SubLaunch& a, hipStream_t s) {
 hipError_t launch_sub_apply(const SubLaunch& a, hipStream_t s) {
   if (a.n_slots <= 0 || a.n_samples <= 0) return hipSuccess;
   dim3 g2((unsigned)((a.n_samples + kApTile - 1) / kApTile), (unsigned)a.n_slots);
-  const size_t lds2 = (size_t)a.nsps * sizeof(float4);
+  const size_t lds2 = (size_t)a.nsps * sizeof(float4) + (size_t)(a.nsps / 8) * sizeof(float);
   hipError_t e = hipSuccess;
   if (a.dtype == FT8_I16) {
     if ((e = allow_lds(k_sub_apply<int16_t>, lds2)) != hipSuccess) return e;
-    hipLaunchKernelGGL(k_sub_apply<int16_t>, g2, dim3(kSubThreads), lds2, s, a);
+    hipLaunchKernelGGL(k_sub_apply<int16_t>, g2, dim3(kApThreads), lds2, s, a);
   } else {
     if ((e = allow_lds(k_sub_apply<float>, lds2)) != hipSuccess) return e;
-    hipLaunchKernelGGL(k_sub_apply<float>, g2, dim3(kSubThreads), lds2, s, a);
+    hipLaunchKernelGGL(k_sub_apply<float>, g2, dim3(kApThreads), lds2, s, a);
   }
   return hipGetLastError();
 }

@@ -7,10 +7,11 @@
 // in np.float32 (NumPy-2 promotion, ft8_decode.py:57,80-94) and any re-association would change
 // the last bit of the score, so the sum is never tree-reduced.
 //
-// k_score2 (float32 waterfall, bins_per_tone/steps_per_symbol in {1..4}, the production path):
-//   * a workgroup owns 128 frequency columns x 22 time rows of the grid of one slot; it stages the
-//     three Costas bands of the waterfall those candidates touch (3 x (22 + 8 sps) rows x
-//     (128 + 7 bpt) columns, 63 KB at bpt = sps = 2) in LDS once;
+// k_score2 (float32 waterfall, bins_per_tone = steps_per_symbol in {1..4, 10}, the production path):
+//   * a workgroup owns 128 frequency columns x 22 time rows of the grid of one slot, the rows one
+//     residue class mod sps; it stages the three Costas bands of the waterfall those candidates
+//     touch one at a time ((22 + 8) rows of stride sps x (128 + 7 bpt) columns, 17 KB at
+//     bpt = sps = 2) in LDS;
 //   * a wave owns one time row at a time (so every range test of the reference is wave-uniform and
 //     compiles to a scalar branch) and each lane two adjacent columns: the pair is accumulated
 //     with packed float32 adds (v_pk_add_f32, two independent IEEE sums) from 8-byte LDS reads
@@ -181,10 +182,15 @@ constexpr int kS2Rows = (kS2R + kS2Waves - 1) / kS2Waves;  // rows per wave (3, 
 constexpr int kS2Threads = kS2Waves * kWave;
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
+// A workgroup's 22 grid rows are one residue class mod sps, consecutive in it: abs_time a0 +
+// sps j, j < 22.  Every waterfall row those candidates read for Costas band m is a0 + 36 m sps +
+// sps (j + k + d) (symbol k, time neighbour d = -1, 0, 1), so the band's tile is 22 + 8 rows of
+// stride sps -- one tile row per symbol step, whatever sps is -- instead of 22 + 8 sps consecutive
+// rows, most of them unread (at sps = 10, 102 rows for 30 used; sps = 2: 38 for 30).
 template <int BPT, int SPS>
 struct S2Geom {
   static constexpr int P = (kS2TW + 7 * BPT + 3) & ~3;   // staged columns (multiple of 4: float4 rows)
-  static constexpr int H = kS2R + 8 * SPS;               // staged rows of one Costas band
+  static constexpr int H = kS2R + 8;                     // staged rows of one Costas band
   static constexpr int kFloats = H * P;                  // the LDS tile: one band at a time
   static constexpr int Q = P / 4;                        // float4 per staged row
   static constexpr int kIter = (H * Q + kS2Threads - 1) / kS2Threads;  // float4 staged per thread
@@ -221,9 +227,9 @@ __device__ __forceinline__ f32x2 ld2(const float* p) {
   else return f32x2{p[0], p[1]};
 }
 
-// Costas band m of the tile (staged rows [a0 - SPS + 36 m SPS, + H), columns [c0, c0 + P)) as float4
-// loads into registers; rows outside the waterfall / columns past F are zero and never read by a
-// valid candidate.  Thread t owns float4 t + 512 it.
+// Costas band m of the tile (staged rows a0 - SPS + 36 m SPS + SPS u, u < H; columns [c0, c0 + P))
+// as float4 loads into registers; rows outside the waterfall / columns past F are zero and never
+// read by a valid candidate.  Thread t owns float4 t + 512 it.
 template <int BPT, int SPS>
 __device__ __forceinline__ void s2_load(const float* wf, int T, int F, int a0, int c0, int m,
                                         float4 (&v)[S2Geom<BPT, SPS>::kIter]) {
@@ -232,16 +238,17 @@ __device__ __forceinline__ void s2_load(const float* wf, int T, int F, int a0, i
   for (int it = 0; it < G::kIter; ++it) {
     const int idx = (int)threadIdx.x + it * kS2Threads;
     const int rw = idx / G::Q, q4 = idx - rw * G::Q;
-    const int row = a0 - SPS + 36 * m * SPS + rw, col = c0 + 4 * q4;
+    const int row = a0 - SPS + 36 * m * SPS + SPS * rw, col = c0 + 4 * q4;
     v[it] = make_float4(0.f, 0.f, 0.f, 0.f);
     if (idx < G::H * G::Q && row >= 0 && row < T && col < F)
       v[it] = *reinterpret_cast<const float4*>(wf + (int64_t)row * F + col);
   }
 }
 
-// One workgroup: 128 grid columns x 22 grid rows of one slot.  The three Costas bands of the
-// waterfall the candidates read are staged into LDS ONE AT A TIME (22 KB at bpt = sps = 2, so four
-// workgroups -- 32 waves -- share a CU), band m + 1's global loads in flight while band m is scored;
+// One workgroup: 128 grid columns x 22 grid rows of one slot (one residue class mod sps, above).
+// The three Costas bands of the waterfall the candidates read are staged into LDS ONE AT A TIME
+// (17 KB at bpt = sps = 2, 24 KB at bpt = sps = 10), band m + 1's global loads in flight while band m
+// is scored;
 // each wave keeps its rows' two-column partial sums in registers across the bands, so every score
 // still accumulates its 75 terms in the reference's order (band, symbol, tone-1, tone+1, time-1,
 // time+1).
@@ -261,7 +268,12 @@ __global__ __launch_bounds__(kS2Threads) void k_score2(ScoreArgs a) {
   if (slot >= a.n_slots) return;
   const int r = q % per;
   const int band = r / a.n_ctiles, ct = r - band * a.n_ctiles;
-  const int a0 = a.t0 + band * kS2R;
+  // band -> (residue class c of the grid rows mod SPS, 22-row tile b of the class)
+  const int nbpc = a.n_bands / SPS;
+  const int cls = band / nbpc, i0 = (band - cls * nbpc) * kS2R;
+  const int cnt = (a.NT - cls + SPS - 1) / SPS;  // grid rows of the class
+  if (i0 >= cnt) return;                          // (workgroup-uniform)
+  const int a0 = a.t0 + cls + SPS * i0;           // abs_time of the tile's first candidate row
   const int c0 = ct * kS2TW;
   const float* wf = reinterpret_cast<const float*>(a.wf) + (int64_t)slot * a.T * a.F;
   const bool vec = (a.F & 3) == 0;
@@ -270,7 +282,7 @@ __global__ __launch_bounds__(kS2Threads) void k_score2(ScoreArgs a) {
   const int lane = threadIdx.x & 63;
   const int af = c0 + 2 * lane;
   const int nb = a.num_blocks;
-  const int rows = min(kS2R, a.t0 + a.NT - a0);
+  const int rows = min(kS2R, cnt - i0);
   f32x2 score[kS2Rows];
   int n[kS2Rows];
 #pragma unroll
@@ -294,7 +306,7 @@ __global__ __launch_bounds__(kS2Threads) void k_score2(ScoreArgs a) {
     } else {
       for (int i = threadIdx.x; i < G::kFloats; i += kS2Threads) {
         const int rr = i / P, cc = i - rr * P;
-        const int row = a0 + 36 * m * SPS - SPS + rr, col = c0 + cc;
+        const int row = a0 + 36 * m * SPS - SPS + SPS * rr, col = c0 + cc;
         float x = 0.0f;
         if (row >= 0 && row < a.T && col < a.F) x = wf[(int64_t)row * a.F + col];
         tile[i] = x;
@@ -305,20 +317,21 @@ __global__ __launch_bounds__(kS2Threads) void k_score2(ScoreArgs a) {
     for (int u = 0; u < kS2Rows; ++u) {
       const int j = w + u * kS2Waves;        // wave-uniform
       if (j >= rows) continue;
-      const int lo = floordiv(a0 + j, SPS) + 36 * m;  // block index of the band's first Costas symbol
-      const float* tb = tile + j * P + 2 * lane;
+      // block index of the band's first Costas symbol for abs_time a0 + SPS j
+      const int lo = floordiv(a0, SPS) + j + 36 * m;
+      const float* tb = tile + j * P + 2 * lane;  // tile row j + k + 1: symbol k, +-1: time neighbours
       if (lo >= 0 && lo <= nb - 7) {
         // every symbol of the band and all its neighbours in range: straight-line code
         // (25 differences, in the reference order)
 #pragma unroll
         for (int k = 0; k < 7; ++k) {
           const int tone = kCostasC[k];
-          const float* rp = tb + (k + 1) * SPS * P + tone * BPT;
+          const float* rp = tb + (k + 1) * P + tone * BPT;
           const f32x2 pw = ld2<BPT>(rp);
           if (tone > 0) score[u] += pw - ld2<BPT>(rp - BPT);
           if (tone < 7) score[u] += pw - ld2<BPT>(rp + BPT);
-          if (k > 0) score[u] += pw - ld2<BPT>(rp - SPS * P);
-          if (k < 6) score[u] += pw - ld2<BPT>(rp + SPS * P);
+          if (k > 0) score[u] += pw - ld2<BPT>(rp - P);
+          if (k < 6) score[u] += pw - ld2<BPT>(rp + P);
         }
         n[u] += 25;
       } else if (lo + 6 >= 0 && lo < nb) {
@@ -328,12 +341,12 @@ __global__ __launch_bounds__(kS2Threads) void k_score2(ScoreArgs a) {
           const int ba = lo + k;
           if (ba < 0 || ba >= nb) continue;
           const int tone = kCostasC[k];
-          const float* rp = tb + (k + 1) * SPS * P + tone * BPT;
+          const float* rp = tb + (k + 1) * P + tone * BPT;
           const f32x2 pw = ld2<BPT>(rp);
           if (tone > 0) { score[u] += pw - ld2<BPT>(rp - BPT); n[u]++; }
           if (tone < 7) { score[u] += pw - ld2<BPT>(rp + BPT); n[u]++; }
-          if (k > 0 && ba > 0) { score[u] += pw - ld2<BPT>(rp - SPS * P); n[u]++; }
-          if (k < 6 && ba + 1 < nb) { score[u] += pw - ld2<BPT>(rp + SPS * P); n[u]++; }
+          if (k > 0 && ba > 0) { score[u] += pw - ld2<BPT>(rp - P); n[u]++; }
+          if (k < 6 && ba + 1 < nb) { score[u] += pw - ld2<BPT>(rp + P); n[u]++; }
         }
       }
     }
@@ -351,7 +364,7 @@ __global__ __launch_bounds__(kS2Threads) void k_score2(ScoreArgs a) {
       const float sc = score[u][c];
       res[c] = (n[u] == 0 || isnan(sc) || isinf(sc)) ? -INFINITY : sc / (float)n[u];
     }
-    const int ti = a0 + j - a.t0;
+    const int ti = a0 + SPS * j - a.t0;
     const bool v0 = af < a.NF, v1 = af + 1 < a.NF;
     const bool p0 = v0 && passes(res[0], a.min_score, a.cmp_f64);
     const bool p1 = v1 && passes(res[1], a.min_score, a.cmp_f64);
@@ -388,14 +401,15 @@ template <int BPT, int SPS, bool COMPACT>
 hipError_t launch_score2(const SyncLaunch& L, const ScoreArgs& a0, hipStream_t s) {
   using G = S2Geom<BPT, SPS>;
   ScoreArgs a = a0;
-  a.n_bands = (L.NT + kS2R - 1) / kS2R;
+  // SPS residue classes of the grid rows, each cut into 22-row tiles (classes hold ceil(NT / SPS)
+  // rows at most; a tile past its class's rows exits at once)
+  a.n_bands = SPS * ((((L.NT + SPS - 1) / SPS) + kS2R - 1) / kS2R);
   a.n_ctiles = (L.NF + kS2TW - 1) / kS2TW;
   const size_t lds = sizeof(float) * G::kFloats;
   static_assert(sizeof(float) * S2Geom<4, 4>::kFloats <= 64 * 1024, "one band fits the default LDS limit");
   static_assert(sizeof(float) * G::kFloats <= 160 * 1024, "one band fits the CU's LDS");
   if constexpr (sizeof(float) * G::kFloats > 64 * 1024) {
-    // bpt = sps = 10 (the reference decode test's geometry): a band is 102 rows x 200 columns,
-    // 82 KB -- one workgroup per CU, still far from the generic kernel's uncached row reads
+    // (no geometry built today needs it: bpt = sps = 10's band is 30 rows x 200 columns, 24 KB)
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k_score2<BPT, SPS, COMPACT>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;

@@ -99,3 +99,15 @@ def test_counters_for_build_takes_headline_passes_only(tmp_path, monkeypatch):
     assert src == "profiles/r4_v23_pmc_traffic.json" and k["k"]["from"] == "r4_v23_pmc_traffic.json"
     k, src = bench.counters_for_build("r*_pmc_traffic.json", "C")
     assert k is None and src.startswith("stale: profiles/r4_v23_pmc_traffic.json")
+
+
+def test_bp_cpu_baseline_threads(bench):
+    """bench.bp_cpu_baseline (bp_stress's CPU leg): every sample vector decoded, rate and
+    extrapolation reported with the thread count."""
+    from oracle import oracle as O
+    rng = np.random.default_rng(5)
+    xn = np.stack([O.normalize(rng.standard_normal(174) * 2.0) for _ in range(24)])
+    out = bench.bp_cpu_baseline(xn, 5, 3, 100000)
+    assert out["cores"] == 3 and out["kind"] == "port" and out["value"] > 0
+    assert out["extrapolated_s_per_launch"] == 100000 / out["value"]
+    assert out["sample"].startswith("24 of")
