@@ -328,9 +328,11 @@ struct BpArgs {
   ft8_result* res;
   unsigned long long* work;   // claim counter (64-bit, never reset)
   unsigned long long work_base;  // this launch's first ticket (BpLaunch.work_base)
-  unsigned long long* stats;  // nullable: [candidates, iterations entered, message passes, converged]
-  unsigned long long* clock;  // nullable (timed launches only): [sum of wave shader-clock cycles,
-                              //  sum of wave wall-clock ticks, max wave cycles, waves] (ft8_get_bp_clock)
+  unsigned long long* stats;  // nullable: per row (kStatRows x kStatStride) [candidates, iterations
+                              //  entered, message passes, converged]
+  unsigned long long* clock;  // nullable (timed launches only), stats + 4: per row [sum of wave
+                              //  shader-clock cycles, sum of wave wall-clock ticks, max wave cycles,
+                              //  waves] (ft8_get_bp_clock)
   int slot0;
   int tie_blocks;             // k_llr's first tie_blocks workgroups run tie_order
   TieArgs tie;
@@ -437,125 +439,185 @@ __global__ __launch_bounds__(kWave) void k_tie_apply(TieArgs a, int32_t* cand, d
   }
 }
 
-// numpy pairwise sum (loops_utils.h.src) of x[0..174): pw(0,80) + pw(80,94), result in lane 0
-__device__ double pairwise174(const double* x, double* part, int lane) {
-  if (lane < 8) {
-    double r = x[lane];
-    for (int i = 8; i < 80; i += 8) r += x[i + lane];
-    part[lane] = r;
-  } else if (lane < 16) {
-    const int j = lane - 8;
-    double r = x[80 + j];
-    for (int i = 8; i < 88; i += 8) r += x[80 + i + j];
-    part[lane] = r;
+constexpr int kLlrCpw = 4;                  // k_llr: candidates per wave
+constexpr int kLlrRow = FT8_LDPC_N + 2;     // LDS row of one candidate's 174 doubles (padded)
+
+// numpy pairwise sum (loops_utils.h.src) of x[u][0..174) for the wave's kLlrCpw candidates at once:
+// pw(0,80) + pw(80,94).  Lanes 16 u + l hold candidate u's 16 partial sums (l < 8: the 8
+// accumulators of [0, 80), l >= 8: those of [80, 168)), lane 16 u combines them with the tail
+// [168, 174) in numpy's order; every lane receives its candidate's sum.  (One candidate per wave,
+// as in round 4, kept 48 of the 64 lanes idle through both sums of the normalisation.)
+__device__ double pairwise174x4(const double (*x)[kLlrRow], double (*part)[16], int lane) {
+  const int u = lane >> 4, l = lane & 15;
+  const double* xu = x[u];
+  double r;
+  if (l < 8) {
+    r = xu[l];
+    for (int i = 8; i < 80; i += 8) r += xu[i + l];
+  } else {
+    const int j = l - 8;
+    r = xu[80 + j];
+    for (int i = 8; i < 88; i += 8) r += xu[80 + i + j];
   }
+  part[u][l] = r;
   __syncthreads();
   double tot = 0.0;
-  if (lane == 0) {
-    const double s1 = ((part[0] + part[1]) + (part[2] + part[3])) + ((part[4] + part[5]) + (part[6] + part[7]));
-    double s2 = ((part[8] + part[9]) + (part[10] + part[11])) + ((part[12] + part[13]) + (part[14] + part[15]));
-    for (int i = 168; i < 174; ++i) s2 += x[i];
+  if (l == 0) {
+    const double* pu = part[u];
+    const double s1 = ((pu[0] + pu[1]) + (pu[2] + pu[3])) + ((pu[4] + pu[5]) + (pu[6] + pu[7]));
+    double s2 = ((pu[8] + pu[9]) + (pu[10] + pu[11])) + ((pu[12] + pu[13]) + (pu[14] + pu[15]));
+    for (int i = 168; i < 174; ++i) s2 += xu[i];
     tot = 0.0 + (s1 + s2);  // add.reduce starts from the identity
   }
   __syncthreads();
-  return __shfl(tot, 0);
+  return __shfl(tot, lane & ~15);
 }
 
-// ft8_extract_likelihood (ft8_decode.py:164-188) with the gathers spread over the wave: lane 8 g + i fetches tone i of symbol 8 r + g in
-// round r, so one load instruction covers 8 symbols' rows (one or two cache lines each) instead of
-// 58 rows -- a candidate costs ~8x fewer L1 tag lookups -- and the tone powers reach their symbol's
-// lane through LDS (stage: 64 symbols x 8 tones).
+// ft8_extract_likelihood (ft8_decode.py:164-188) of the wave's candidates with the gathers spread over
+// the wave: lane 8 g + i fetches tone i of symbol 8 r + g in round r, so one load instruction covers
+// 8 symbols' rows (one or two cache lines each) instead of 58 rows; the loads of all kLlrCpw
+// candidates are issued before the first is used (32 in flight per lane), and the tone powers reach
+// their symbol's lane through LDS (stage: 64 symbols x 8 tones per candidate).
 template <typename T>
-__device__ void extract_llr_coop(const BpArgs& a, const T* wf, int at, int af, double* c, T* stage, int lane) {
+__device__ void extract_llr_x4(const BpArgs& a, const int (&slot)[kLlrCpw], const int (&at)[kLlrCpw],
+                               const int (&af)[kLlrCpw], int n_on, double (*c)[kLlrRow], T (*stage)[64 * 8],
+                               int lane) {
   const int i = lane & 7, g = lane >> 3;
-  const int base = floordiv(at, a.sps);
-  T v[8];
+  const T* wf0 = reinterpret_cast<const T*>(a.wf);
+  T v[kLlrCpw][8];
 #pragma unroll
-  for (int r = 0; r < 8; ++r) {
-    const int k = 8 * r + g;
-    const int sym = k + (k < 29 ? 7 : 14);
-    const int block = base + sym;
-    v[r] = (T)0;
-    if (k < 58 && !(block < 0 || block >= a.num_blocks))
-      v[r] = wf[(int64_t)(at + sym * a.sps) * a.F + af + i * a.bpt];
+  for (int u = 0; u < kLlrCpw; ++u) {
+    const int base = floordiv(at[u], a.sps);
+    const T* wf = wf0 + (int64_t)slot[u] * a.T * a.F;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const int k = 8 * r + g;
+      const int sym = k + (k < 29 ? 7 : 14);
+      const int block = base + sym;
+      v[u][r] = (T)0;
+      if (u < n_on && k < 58 && !(block < 0 || block >= a.num_blocks))
+        v[u][r] = wf[(int64_t)(at[u] + sym * a.sps) * a.F + af[u] + i * a.bpt];
+    }
   }
 #pragma unroll
-  for (int r = 0; r < 8; ++r) stage[8 * (8 * r + g) + i] = v[r];
+  for (int u = 0; u < kLlrCpw; ++u)
+#pragma unroll
+    for (int r = 0; r < 8; ++r) stage[u][8 * (8 * r + g) + i] = v[u][r];
   __syncthreads();
   if (lane < 58) {
     const int k = lane;
     const int sym = k + (k < 29 ? 7 : 14);
-    const int block = base + sym;
-    double l0 = 0.0, l1 = 0.0, l2 = 0.0;
-    if (!(block < 0 || block >= a.num_blocks)) {
-      double s[8], s2[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) s[j] = (double)stage[8 * k + j];
+    for (int u = 0; u < kLlrCpw; ++u) {
+      if (u >= n_on) break;
+      const int block = floordiv(at[u], a.sps) + sym;
+      double l0 = 0.0, l1 = 0.0, l2 = 0.0;
+      if (!(block < 0 || block >= a.num_blocks)) {
+        double s[8], s2[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) s2[j] = s[kGrayD[j]];
-      l0 = pymax4(s2[4], s2[5], s2[6], s2[7]) - pymax4(s2[0], s2[1], s2[2], s2[3]);
-      l1 = pymax4(s2[2], s2[3], s2[6], s2[7]) - pymax4(s2[0], s2[1], s2[4], s2[5]);
-      l2 = pymax4(s2[1], s2[3], s2[5], s2[7]) - pymax4(s2[0], s2[2], s2[4], s2[6]);
+        for (int j = 0; j < 8; ++j) s[j] = (double)stage[u][8 * k + j];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s2[j] = s[kGrayD[j]];
+        l0 = pymax4(s2[4], s2[5], s2[6], s2[7]) - pymax4(s2[0], s2[1], s2[2], s2[3]);
+        l1 = pymax4(s2[2], s2[3], s2[6], s2[7]) - pymax4(s2[0], s2[1], s2[4], s2[5]);
+        l2 = pymax4(s2[1], s2[3], s2[5], s2[7]) - pymax4(s2[0], s2[2], s2[4], s2[6]);
+      }
+      c[u][3 * k] = l0;
+      c[u][3 * k + 1] = l1;
+      c[u][3 * k + 2] = l2;
     }
-    c[3 * k] = l0;
-    c[3 * k + 1] = l1;
-    c[3 * k + 2] = l2;
   }
 }
 
-// ---- k_llr: one wave per candidate -> normalised LLRs in global memory ---------------------------
-// modes: 0 per-slot candidate lists (skips ranks >= the slot's count), 1 explicit (slot, t, f) list,
-// 2 normalise given LLRs
+// ---- k_llr: one wave per kLlrCpw candidates -> normalised LLRs in global memory --------------------
+// modes: 0 per-slot candidate lists (4 consecutive ranks of one slot per wave; ranks >= the slot's
+// count skipped), 1 explicit (slot, t, f) list, 2 normalise given LLRs.  Items u = 0 .. n_on - 1 of
+// the wave are item0 + u (the active ones are always a prefix).
 template <typename T>
 __global__ __launch_bounds__(kWave) void k_llr(BpArgs a) {
-  __shared__ double c[FT8_LDPC_N + 2];
-  __shared__ double sq[FT8_LDPC_N + 2];
-  __shared__ double part[16];
+  __shared__ double c[kLlrCpw][kLlrRow];
+  __shared__ double part[kLlrCpw][16];
+  __shared__ double bc[kLlrCpw];
+  // the gather stage (extraction) and the squared deviations (normalisation) share one buffer: a
+  // barrier separates the two uses, and the LDS per wave sets how many waves a CU holds
+  constexpr size_t kScratch = sizeof(T) * kLlrCpw * 64 * 8 > sizeof(double) * kLlrCpw * kLlrRow
+                                  ? sizeof(T) * kLlrCpw * 64 * 8 : sizeof(double) * kLlrCpw * kLlrRow;
+  __shared__ __attribute__((aligned(16))) unsigned char scratch[kScratch];
+  double (*sq)[kLlrRow] = reinterpret_cast<double (*)[kLlrRow]>(scratch);
   const int lane = threadIdx.x;
   if ((int)blockIdx.x < a.tie_blocks) {
     tie_order(a.tie, blockIdx.x);
     return;
   }
   const int id = blockIdx.x - a.tie_blocks;  // tie_blocks % 8 == 0 keeps id % 8 == XCD
-  int item = id;
-  int slot = 0, at = 0, af = 0;
+  int item0, n_on;
+  int slot[kLlrCpw] = {0, 0, 0, 0}, at[kLlrCpw] = {0, 0, 0, 0}, af[kLlrCpw] = {0, 0, 0, 0};
+  static_assert(kLlrCpw == 4, "four candidates per wave");
   if (a.mode == 0) {
-    // workgroup id -> (slot, candidate) with slot % 8 == id % 8: all candidates of a slot run on
-    // one XCD, so its waterfall rows are fetched into one L2 (round-robin ids would pull every
-    // slot into all eight)
+    // workgroup id -> (slot, group of 4 ranks) with slot % 8 == id % 8: all candidates of a slot run
+    // on one XCD, so its waterfall rows are fetched into one L2
+    const int groups = (a.N + kLlrCpw - 1) / kLlrCpw;
     const int q = id >> 3;
-    slot = (q / a.N) * 8 + (id & 7);
-    const int cidx = q % a.N;
-    if (slot >= a.n_slots || cidx >= a.cand_count[slot]) return;
-    item = slot * a.N + cidx;
-    at = a.cand[((int64_t)slot * a.N + cidx) * 2];
-    af = a.cand[((int64_t)slot * a.N + cidx) * 2 + 1];
-  } else if (a.mode == 1) {
-    slot = a.cand[(int64_t)item * 3];
-    at = a.cand[(int64_t)item * 3 + 1];
-    af = a.cand[(int64_t)item * 3 + 2];
-  }
-  else if (item >= a.n_items) return;
-  if (a.mode == 2) {
-    for (int n = lane; n < FT8_LDPC_N; n += kWave) c[n] = a.llr_in[(int64_t)item * FT8_LDPC_N + n];
+    const int s0 = (q / groups) * 8 + (id & 7);
+    const int c0 = (q % groups) * kLlrCpw;
+    if (s0 >= a.n_slots) return;
+    n_on = min(kLlrCpw, min(a.N, a.cand_count[s0]) - c0);
+    item0 = s0 * a.N + c0;
+#pragma unroll
+    for (int u = 0; u < kLlrCpw; ++u) {
+      slot[u] = s0;
+      if (u < n_on) {
+        at[u] = a.cand[((int64_t)item0 + u) * 2];
+        af[u] = a.cand[((int64_t)item0 + u) * 2 + 1];
+      }
+    }
   } else {
-    __shared__ T stage[64 * 8];
-    extract_llr_coop<T>(a, reinterpret_cast<const T*>(a.wf) + (int64_t)slot * a.T * a.F, at, af, c, stage, lane);
+    item0 = id * kLlrCpw;
+    n_on = min(kLlrCpw, a.n_items - item0);
+    if (a.mode == 1) {
+#pragma unroll
+      for (int u = 0; u < kLlrCpw; ++u) {
+        if (u < n_on) {
+          slot[u] = a.cand[((int64_t)item0 + u) * 3];
+          at[u] = a.cand[((int64_t)item0 + u) * 3 + 1];
+          af[u] = a.cand[((int64_t)item0 + u) * 3 + 2];
+        }
+      }
+    }
+  }
+  if (n_on <= 0) return;  // wave-uniform
+  if (a.mode == 2) {
+    for (int e = lane; e < n_on * FT8_LDPC_N; e += kWave) {
+      const int u = e / FT8_LDPC_N, n = e - u * FT8_LDPC_N;
+      c[u][n] = a.llr_in[(int64_t)(item0 + u) * FT8_LDPC_N + n];
+    }
+  } else {
+    extract_llr_x4<T>(a, slot, at, af, n_on, c, reinterpret_cast<T (*)[64 * 8]>(scratch), lane);
   }
   __syncthreads();
-  if (a.normalize) {  // ftx_normalize_logl (ft8_decode.py:190-198)
-    const double mean = pairwise174(c, part, lane) / 174.0;
-    for (int n = lane; n < FT8_LDPC_N; n += kWave) {
-      const double d = c[n] - mean;
-      sq[n] = d * d;
+  if (a.normalize) {  // ftx_normalize_logl (ft8_decode.py:190-198), the wave's candidates side by side
+    const double mean = pairwise174x4(c, part, lane) / 174.0;
+    if ((lane & 15) == 0) bc[lane >> 4] = mean;
+    __syncthreads();
+    for (int e = lane; e < n_on * FT8_LDPC_N; e += kWave) {
+      const int u = e / FT8_LDPC_N, n = e - u * FT8_LDPC_N;
+      const double d = c[u][n] - bc[u];
+      sq[u][n] = d * d;
     }
     __syncthreads();
-    const double var = pairwise174(sq, part, lane) / 174.0;
-    const double nf = sqrt_rn(24.0 / var);
-    for (int n = lane; n < FT8_LDPC_N; n += kWave) c[n] = c[n] * nf;
+    const double var = pairwise174x4(sq, part, lane) / 174.0;
+    if ((lane & 15) == 0) bc[lane >> 4] = sqrt_rn(24.0 / var);
     __syncthreads();
+    for (int e = lane; e < n_on * FT8_LDPC_N; e += kWave) {
+      const int u = e / FT8_LDPC_N, n = e - u * FT8_LDPC_N;
+      a.llr_out[(int64_t)(item0 + u) * FT8_LDPC_N + n] = c[u][n] * bc[u];
+    }
+    return;
   }
-  for (int n = lane; n < FT8_LDPC_N; n += kWave) a.llr_out[(int64_t)item * FT8_LDPC_N + n] = c[n];
+  for (int e = lane; e < n_on * FT8_LDPC_N; e += kWave) {
+    const int u = e / FT8_LDPC_N, n = e - u * FT8_LDPC_N;
+    a.llr_out[(int64_t)(item0 + u) * FT8_LDPC_N + n] = c[u][n];
+  }
 }
 
 // Phase boundary inside a sweep.  The workgroup is one wave and the LDS executes a wave's
@@ -950,18 +1012,19 @@ __global__ __launch_bounds__(kWave, kBpLbWaves) void k_bp(BpArgs a) {
     }
     __syncthreads();
   }
+  const unsigned row = (blockIdx.x & (unsigned)(kStatRows - 1)) * (unsigned)kStatStride;
   if (a.stats && lane == 0 && st_cand) {
-    atomicAdd(&a.stats[0], (unsigned long long)st_cand);
-    atomicAdd(&a.stats[1], (unsigned long long)st_iter);
-    atomicAdd(&a.stats[2], (unsigned long long)st_pass);
-    atomicAdd(&a.stats[3], (unsigned long long)st_conv);
+    atomicAdd(&a.stats[row + 0], (unsigned long long)st_cand);
+    atomicAdd(&a.stats[row + 1], (unsigned long long)st_iter);
+    atomicAdd(&a.stats[row + 2], (unsigned long long)st_pass);
+    atomicAdd(&a.stats[row + 3], (unsigned long long)st_conv);
   }
   if (a.clock && lane == 0) {
     const unsigned long long cyc = clock64() - clk0, wall = wall_clock64() - wall0;
-    atomicAdd(&a.clock[0], cyc);
-    atomicAdd(&a.clock[1], wall);
-    atomicMax(&a.clock[2], cyc);
-    atomicAdd(&a.clock[3], 1ull);
+    atomicAdd(&a.clock[row + 0], cyc);
+    atomicAdd(&a.clock[row + 1], wall);
+    atomicMax(&a.clock[row + 2], cyc);
+    atomicAdd(&a.clock[row + 3], 1ull);
   }
 }
 
@@ -1128,7 +1191,8 @@ BpArgs make_args(const BpLaunch& L) {
 hipError_t launch_llr(const BpLaunch& L, hipStream_t s) {
   if (L.n_items <= 0) return hipSuccess;
   BpArgs a = make_args(L);
-  const int64_t grid = a.tie_blocks + (L.mode == 0 ? (int64_t)((L.n_slots + 7) / 8) * 8 * L.N : L.n_items);
+  const int64_t grid = a.tie_blocks + (L.mode == 0 ? (int64_t)((L.n_slots + 7) / 8) * 8 * ((L.N + kLlrCpw - 1) / kLlrCpw)
+                                                    : ((int64_t)L.n_items + kLlrCpw - 1) / kLlrCpw);
   if (L.wf_f64)
     hipLaunchKernelGGL(k_llr<double>, dim3((unsigned)grid), dim3(kWave), 0, s, a);
   else

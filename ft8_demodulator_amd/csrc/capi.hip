@@ -1491,9 +1491,10 @@ int ft8_set_timing(ft8_ctx* c, int enable) {
   c->timing = enable != 0;
   if (c->timing && !c->stats.p) {
     DeviceGuard dg(c->device);
-    int rc = ensure(c, c->stats, 8 * sizeof(unsigned long long));
+    const size_t bytes = (size_t)kStatRows * kStatStride * sizeof(unsigned long long);
+    int rc = ensure(c, c->stats, bytes);
     if (rc) return rc;
-    hipError_t e = hipMemset(c->stats.p, 0, 8 * sizeof(unsigned long long));
+    hipError_t e = hipMemset(c->stats.p, 0, bytes);
     if (e != hipSuccess) return hipfail(c, e, "stats reset");
   }
   return FT8_OK;
@@ -1505,16 +1506,32 @@ int ft8_set_timing_stages(ft8_ctx* c, uint32_t mask) {
   return FT8_OK;
 }
 
+// the k_bp counter rows (kStatRows x kStatStride) summed per column (column 6, the longest wave,
+// by maximum); reset zeroes columns [c0, c0 + 4) of every row
+static int read_stat_rows(ft8_ctx* c, int c0, int reset, unsigned long long* out4) {
+  std::vector<unsigned long long> v((size_t)kStatRows * kStatStride);
+  hipError_t e = hipDeviceSynchronize();
+  if (e == hipSuccess) e = hipMemcpy(v.data(), c->stats.p, v.size() * sizeof(v[0]), hipMemcpyDeviceToHost);
+  if (e == hipSuccess && reset)
+    e = hipMemset2D((char*)c->stats.p + c0 * sizeof(v[0]), kStatStride * sizeof(v[0]), 0, 4 * sizeof(v[0]), kStatRows);
+  if (e != hipSuccess) return hipfail(c, e, "counters");
+  for (int i = 0; i < 4; ++i) out4[i] = 0;
+  for (int r = 0; r < kStatRows; ++r)
+    for (int i = 0; i < 4; ++i) {
+      const unsigned long long x = v[(size_t)r * kStatStride + c0 + i];
+      out4[i] = (c0 + i == 6) ? std::max(out4[i], x) : out4[i] + x;
+    }
+  return FT8_OK;
+}
+
 int ft8_get_counters(ft8_ctx* c, int64_t* out4, int reset) {
   if (!c || !out4) return FT8_E_ARG;
   for (int i = 0; i < 4; ++i) out4[i] = 0;
   if (!c->stats.p) return FT8_OK;
   DeviceGuard dg(c->device);
   unsigned long long v[4];
-  hipError_t e = hipDeviceSynchronize();
-  if (e == hipSuccess) e = hipMemcpy(v, c->stats.p, sizeof(v), hipMemcpyDeviceToHost);
-  if (e == hipSuccess && reset) e = hipMemset(c->stats.p, 0, sizeof(v));
-  if (e != hipSuccess) return hipfail(c, e, "counters");
+  int rc = read_stat_rows(c, 0, reset, v);
+  if (rc) return rc;
   for (int i = 0; i < 4; ++i) out4[i] = (int64_t)v[i];
   return FT8_OK;
 }
@@ -1529,11 +1546,8 @@ int ft8_get_bp_clock(ft8_ctx* c, int64_t* out5, int reset) {
   out5[4] = khz;
   if (!c->stats.p) return FT8_OK;
   unsigned long long v[4];
-  e = hipDeviceSynchronize();
-  unsigned long long* clk = (unsigned long long*)c->stats.p + 4;
-  if (e == hipSuccess) e = hipMemcpy(v, clk, sizeof(v), hipMemcpyDeviceToHost);
-  if (e == hipSuccess && reset) e = hipMemset(clk, 0, sizeof(v));
-  if (e != hipSuccess) return hipfail(c, e, "bp clock");
+  int rc = read_stat_rows(c, 4, reset, v);
+  if (rc) return rc;
   for (int i = 0; i < 4; ++i) out5[i] = (int64_t)v[i];
   return FT8_OK;
 }

@@ -189,6 +189,11 @@ hipError_t launch_score_list(const void* wf, int wf_f64, int T, int F, int sps, 
                              int n, void* out, int32_t* err, hipStream_t s);
 
 // ---- LLR + BP + CRC ------------------------------------------------------------------------
+// k_bp's work / clock counters: kStatRows rows of kStatStride u64 (one 128-B line each); wave w adds
+// to row w % kStatRows and the host sums the rows.  One row for all 4 096 waves put every retiring
+// wave's atomics on the same L2 addresses, where they serialise at the launch's tail.
+constexpr int kStatRows = 256;
+constexpr int kStatStride = 16;   // [0..3] work counters, [4..7] clock (BpLaunch.stats / .clock)
 struct BpLaunch {
   // LLR source: either a waterfall + candidate list, or precomputed LLRs
   const void* wf;          // [n_slots][T][F] or null

@@ -21,6 +21,7 @@
 //            summed in record order (deterministic).
 // k_merge    one wave per slot: pass-2 records with a payload not decoded in pass 1 are appended.
 #include <algorithm>
+#include <type_traits>
 
 #include "tx_device.h"
 
@@ -35,6 +36,9 @@ constexpr int kMaxQ = 32;
 constexpr int kMaxHyp = 1024;
 constexpr int kMaxT = kMaxQ + 3;                // start offsets searched: 2 ceil(Q / (2 sps)) + 1
 constexpr int kMf = 2;                         // tone-0 search: 2 kMf + 1 points over +-bin/2
+// float2 words of k_sub_est's padded baseband rows (-1 .. 81 of Q + 1), rounded up to a 16-B multiple;
+// the decimation's twiddle table [D] follows them
+__host__ __device__ inline int z_words(int Q) { return ((tx::kSymbols + 4) * (Q + 1) + 1) & ~1; }
 
 // the fitted signal of one record: the public ft8_sub_fit (include/ft8hip.h, ft8_subtract_fits)
 using SubEst = ft8_sub_fit;
@@ -151,64 +155,61 @@ __global__ __launch_bounds__(kSubThreads) void k_sub_est(SubLaunch a) {
   const double ftone = (double)(a.f_lo + r.abs_freq) * fs / (double)a.nfft;
   const double fmix = ftone + 3.5 * 6.25;
 
-  // ---- 2. mixed-down, box-car decimated baseband z[m], samples [nb + m D, nb + (m + 1) D).  A
-  // thread owns z[tid + 256 j], j < kZ, two at a time, and loads kDc samples of each before it
-  // accumulates them in sample order (2 kDc loads in flight per round trip: four round trips per
-  // pair at D = 60; round 3's two-sample steps over all of a thread's z took ~60 round trips; 32
-  // samples of each z in flight held 172 VGPRs, 16 hold 108: four waves per SIMD)
+  // ---- 2. mixed-down, box-car decimated baseband z[m], samples [nb + m D, nb + (m + 1) D):
+  // z[m] = w_m sum_i x[nb + m D + i] t_i with t_i = exp(-2 pi i fmix i / fs) (a table of D twiddles
+  // in LDS, each from the exact phase) and w_m = exp(-2 pi i fmix (nb + m D) / fs).  A thread owns
+  // z[tid + 256 j]: two fmas per sample.  (Round 4 rotated a per-z phasor by one complex multiply
+  // per sample, ~20 VALU per sample with its per-sample range tests.)  Records whose window lies
+  // inside the slot (all but the slot's edges) read float32 samples four at a time, unchecked.
   {
     constexpr int kZ = (tx::kSymbols * kMaxQ + 2 * (kMaxQ / 2 + 2) + kSubThreads - 1) / kSubThreads;
-    constexpr int kDc = 16;
     const int64_t nb = s0 - (int64_t)Mg * D;
-    float ss, sc;
-    sincospif((float)(-2.0 * fmix / fs), &ss, &sc);
-    const float2 step = make_float2(sc, ss);
+    float2* s_tw = s_z + z_words(Q);
+    for (int i = threadIdx.x; i < D; i += kSubThreads) {
+      const double cyc = fmix * (double)i / fs;
+      float sn, cs;
+      sincospif((float)(-2.0 * (cyc - floor(cyc))), &sn, &cs);
+      s_tw[i] = make_float2(cs, sn);
+    }
+    __syncthreads();
+    const bool inside = nb >= 0 && nb + (int64_t)Mz * D <= a.n_samples;  // workgroup-uniform
 #pragma unroll 1
-    for (int j0 = 0; j0 < kZ; j0 += 2) {
-      float2 wv[2], acc[2];
-      int m[2];
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        m[q] = threadIdx.x + (j0 + q) * kSubThreads;
-        const int64_t n0 = nb + (int64_t)m[q] * D;
-        const double cyc = fmix * (double)n0 / fs;
-        float ws, wc;
-        sincospif((float)(-2.0 * (cyc - floor(cyc))), &ws, &wc);
-        wv[q] = make_float2(wc, ws);
-        acc[q] = make_float2(0.f, 0.f);
-      }
-      if (m[0] >= Mz) break;
-      for (int i0 = 0; i0 < D; i0 += kDc) {
-        float v[2][kDc];
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-          // samples [n0 + lo, n0 + hi) of this chunk exist: one base pointer, immediate offsets
-          const int64_t n0 = nb + (int64_t)m[q] * D + i0;
-          const bool zok = m[q] < Mz && j0 + q < kZ;
-          const int lo = (int)min<int64_t>(kDc, max<int64_t>(0, -n0));
-          const int hi = zok ? (int)max<int64_t>(0, min<int64_t>(min(kDc, D - i0), a.n_samples - n0)) : 0;
-          const InT* xp = x + n0;
-#pragma unroll
-          for (int u = 0; u < kDc; ++u) {
-            v[q][u] = 0.f;
-            if (u >= lo && u < hi) v[q][u] = ld_sample<InT>(xp, u);
-          }
+    for (int j = 0; j < kZ; ++j) {
+      const int m = threadIdx.x + j * kSubThreads;
+      if (m >= Mz) break;
+      const int64_t n0 = nb + (int64_t)m * D;
+      const InT* xp = x + n0;
+      float ax = 0.f, ay = 0.f;
+      if (std::is_same<InT, float>::value && inside && (D & 3) == 0) {
+        for (int i = 0; i < D; i += 4) {
+          float4 v;
+          __builtin_memcpy(&v, xp + i, sizeof(v));  // 4-byte aligned
+          const float4 t01 = *reinterpret_cast<const float4*>(s_tw + i);
+          const float4 t23 = *reinterpret_cast<const float4*>(s_tw + i + 2);
+          ax = fmaf(v.x, t01.x, ax);
+          ay = fmaf(v.x, t01.y, ay);
+          ax = fmaf(v.y, t01.z, ax);
+          ay = fmaf(v.y, t01.w, ay);
+          ax = fmaf(v.z, t23.x, ax);
+          ay = fmaf(v.z, t23.y, ay);
+          ax = fmaf(v.w, t23.z, ax);
+          ay = fmaf(v.w, t23.w, ay);
         }
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-#pragma unroll
-          for (int u = 0; u < kDc; ++u) {
-            if (i0 + u < D) {
-              acc[q].x += v[q][u] * wv[q].x;
-              acc[q].y += v[q][u] * wv[q].y;
-              wv[q] = make_float2(wv[q].x * step.x - wv[q].y * step.y, wv[q].x * step.y + wv[q].y * step.x);
-            }
+      } else {
+        for (int i = 0; i < D; ++i) {
+          const int64_t n = n0 + i;
+          if (n >= 0 && n < a.n_samples) {
+            const float v = ld_sample<InT>(xp, i);
+            const float2 t = s_tw[i];
+            ax = fmaf(v, t.x, ax);
+            ay = fmaf(v, t.y, ay);
           }
         }
       }
-#pragma unroll
-      for (int q = 0; q < 2; ++q)
-        if (m[q] < Mz && j0 + q < kZ) s_z[z_at(m[q])] = acc[q];
+      const double cyc = fmix * (double)n0 / fs;
+      float ws, wc;
+      sincospif((float)(-2.0 * (cyc - floor(cyc))), &ws, &wc);
+      s_z[z_at(m)] = make_float2(ax * wc - ay * ws, ax * ws + ay * wc);
     }
   }
   __syncthreads();
@@ -339,31 +340,34 @@ __global__ __launch_bounds__(kSubThreads) void k_sub_est(SubLaunch a) {
           ay -= vr * sn;
           rr += rp * rp;
         }
-      } else
-      for (int i0 = lane; i0 < nsps; i0 += kPf * kWave) {
-        float v[kPf];
-        const InT* xp = x + nsym + i0;
+      } else {
+        // rp = 1: vr = v * 1, and sum rp^2 is the number of samples the symbol has in the slot (a sum
+        // of 1.0s is exact in any order, so it is that count, not a per-sample add); inside the
+        // slot (wave-uniform, all but the slot's edges) the samples are read without range tests
+        const int64_t lo_n = max<int64_t>(nsym, 0), hi_n = min<int64_t>(nsym + nsps, a.n_samples);
+        rr = (lane == 0 && hi_n > lo_n) ? (float)(hi_n - lo_n) : 0.f;
+        for (int i0 = lane; i0 < nsps; i0 += kPf * kWave) {
+          float v[kPf];
+          const InT* xp = x + nsym + i0;
 #pragma unroll
-        for (int u = 0; u < kPf; ++u) {
-          const int i = i0 + u * kWave;
-          const int64_t n = nsym + i;
-          v[u] = 0.f;
-          if (i < nsps && (inside || (n >= 0 && n < a.n_samples))) v[u] = ld_sample<InT>(xp, u * kWave);
-        }
+          for (int u = 0; u < kPf; ++u) {
+            const int i = i0 + u * kWave;
+            const int64_t n = nsym + i;
+            v[u] = 0.f;
+            if (i < nsps && (inside || (n >= 0 && n < a.n_samples))) v[u] = ld_sample<InT>(xp, u * kWave);
+          }
 #pragma unroll
-        for (int u = 0; u < kPf; ++u) {
-          const int i = i0 + u * kWave;
-          const int64_t n = nsym + i;
-          if (i >= nsps || !(inside || (n >= 0 && n < a.n_samples))) continue;
-          const float4 dd = s_D[i];  // the change of G over the symbol's first i samples
-          const float cyc = ph + (float)i * f0r + sr * (E0 * dd.x + E1 * dd.y + E2 * dd.z);
-          const float fr = __builtin_amdgcn_fractf(cyc);  // v_sin / v_cos take revolutions
-          const float sn = __builtin_amdgcn_sinf(fr), cs = __builtin_amdgcn_cosf(fr);
-          // rp = 1: vr = v * 1 and rr += 1 * 1, the same values as the ramped form
-          const float vr = v[u];
-          ax += vr * cs;
-          ay -= vr * sn;
-          rr += 1.0f;
+          for (int u = 0; u < kPf; ++u) {
+            const int i = i0 + u * kWave;
+            if (i >= nsps) continue;
+            const float4 dd = s_D[i];  // the change of G over the symbol's first i samples
+            const float cyc = ph + (float)i * f0r + sr * (E0 * dd.x + E1 * dd.y + E2 * dd.z);
+            const float fr = __builtin_amdgcn_fractf(cyc);  // v_sin / v_cos take revolutions
+            const float sn = __builtin_amdgcn_sinf(fr), cs = __builtin_amdgcn_cosf(fr);
+            const float vr = v[u];  // 0 outside the slot: adds +-0, as the skipped sample did
+            ax += vr * cs;
+            ay -= vr * sn;
+          }
         }
       }
 #pragma unroll
@@ -614,7 +618,8 @@ hipError_t launch_sub_est(const SubLaunch& a, hipStream_t s) {
     // the rest launch: 8 workgroups per slot that exit at once unless the slot holds more than
     // kSubRecStride fits
     const unsigned grid_rest = (unsigned)(((a.n_slots + 7) / 8) * 8 * (int64_t)kSubRestStride);
-    const size_t mz = (size_t)(tx::kSymbols + 4) * (a.Q + 1);  // padded z rows -1 .. 81 (k_sub_est)
+    // padded z rows -1 .. 81 and the decimation's twiddles (phases 2-3), then the pulse table (phase 4)
+    const size_t mz = (size_t)z_words(a.Q) + (size_t)(a.nsps / a.Q);
     const size_t lds = std::max(mz * sizeof(float2), (size_t)a.nsps * sizeof(float4));
     hipError_t e = hipSuccess;
     if (a.dtype == FT8_I16) {
