@@ -237,9 +237,9 @@ template <typename InT, bool FULL>
 __global__ __launch_bounds__(kThreads38, 4) void k_stft3840p(Args a) {
   FT8_RACE_PROLOGUE();
   __shared__ f2 buf[2][kBuf];  // frame A, frame B
-#ifndef S38_WIN_GLOBAL
-  __shared__ f2 wl[kP / 2];    // the window as pairs (w[2n], w[2n+1]): 39.4 KB in all, four workgroups per CU
-#endif
+  // the window as pairs (w[2n], w[2n+1]) (round 5: read from L1 every pass instead -- 32.6 KB of
+  // LDS -- measured 0.160 vs 0.149 ms per 256-slot launch, profiles/r5_d_ab.log; not kept)
+  __shared__ f2 wl[kP / 2];
   const int t = threadIdx.x;
   // stages 1 and 3: the frame this thread works on (A = 0, B = 1); wave-uniform, so in an SGPR
   const int role = __builtin_amdgcn_readfirstlane(t >> 7);
@@ -268,9 +268,7 @@ __global__ __launch_bounds__(kThreads38, 4) void k_stft3840p(Args a) {
   const f2 pstep = a.post[full ? 128 : kThreads38];
   const f2 qscale = splat(0.25f * a.scale);  // |2 X|^2 / 4 / (sum w)^2 (powers of two: exact)
 
-#ifndef S38_WIN_GLOBAL
   for (int n = t; n < kP / 2; n += kThreads38) wl[n] = *reinterpret_cast<const f2*>(a.window + 2 * n);
-#endif
   const bool s1 = u < 120;
   const InT* xs = reinterpret_cast<const InT*>(a.samples) + (int64_t)slot * a.slot_stride;
   // raw pairs (x[2n], x[2n+1]), n = u + 120 r, of this thread's frame of the pass; loaded for the
@@ -292,15 +290,8 @@ __global__ __launch_bounds__(kThreads38, 4) void k_stft3840p(Args a) {
     __syncthreads();  // the previous pass's epilogue has finished reading both images
     if (s1 && mine) {
       f2 z[8], y[16];
-#ifdef S38_WIN_GLOBAL
-      const f2* wg = reinterpret_cast<const f2*>(a.window);
-      asm volatile("" : "+s"(wg));  // re-read every pass (L1), not hoisted into 16 live VGPRs
-#pragma unroll
-      for (int r = 0; r < 8; ++r) z[r] = wg[u + 120 * r] * raw[r];
-#else
 #pragma unroll
       for (int r = 0; r < 8; ++r) z[r] = lds_ld(&wl[u + 120 * r]) * raw[r];
-#endif
       dft16_half(z, y);
 #pragma unroll
       for (int k = 0; k < 16; ++k) lds_st(&img[17 * u + k], y[k]);  // pidx(16 u + k)

@@ -103,7 +103,6 @@ __global__ __launch_bounds__(kSubThreads) void k_sub_est(SubLaunch a) {
   float2* s_z = reinterpret_cast<float2*>(s_dyn);
   float4* s_D = s_dyn;  // phase 4: the pulse table's symbol-relative differences (see k_sub_apply)
   __shared__ float s_metric[kMaxHyp];
-  __shared__ float2 s_st[(2 * kMf + 1) * 8];
   __shared__ int s_E[tx::kExt];
   __shared__ int s_PS[tx::kExt + 1];
   __shared__ uint8_t s_tones[80];
@@ -220,13 +219,18 @@ __global__ __launch_bounds__(kSubThreads) void k_sub_est(SubLaunch a) {
   const double fstep = 0.5 * bin / kMf;
   const int nT = 2 * Mt + 1, nF = 2 * Mf + 1;
   const int H = min(nT * nF, kMaxHyp);
-  // per-(tone-0 offset, tone) rotation of one decimated sample, staged once
-  if (threadIdx.x < nF * 8) {
-    const int t = threadIdx.x & 7, dfi = (int)threadIdx.x / 8 - Mf;
+  // per-(tone-0 offset, tone) rotation of one decimated sample and its powers w^q, q <= Q, each from
+  // its exact phase (one LDS read and four fmas per sample of a coherent window; round 4 advanced
+  // w^q by a complex multiply per sample)
+  float2* s_W = s_z + z_words(Q) + ((D + 1) & ~1);  // after the twiddles of phase 2: [nF * 8][Q + 1]
+  for (int e = threadIdx.x; e < nF * 8 * (Q + 1); e += kSubThreads) {
+    const int ft = e / (Q + 1), q = e - ft * (Q + 1);
+    const int t = ft & 7, dfi = ft / 8 - Mf;
     const double nu = (double)t * 6.25 + dfi * fstep - 3.5 * 6.25;  // Hz relative to fmix
+    const double cyc = nu * (double)D * (double)q / fs;
     float s_, c_;
-    sincospif((float)(-2.0 * nu * D / fs), &s_, &c_);
-    s_st[threadIdx.x] = make_float2(c_, s_);
+    sincospif((float)(-2.0 * (cyc - floor(cyc))), &s_, &c_);
+    s_W[e] = make_float2(c_, s_);
   }
   __syncthreads();
   // sliding windows: a wave owns one tone-0 offset at a time and a lane one symbol (k, k + 64);
@@ -240,14 +244,14 @@ __global__ __launch_bounds__(kSubThreads) void k_sub_est(SubLaunch a) {
 #pragma unroll
       for (int d = 0; d < kMaxT; ++d) msum[d] = 0.f;
       for (int k = lane; k < tx::kSymbols; k += kWave) {
-        const float2 w = s_st[f * 8 + s_tones[k]];
+        const float2* Wp = s_W + (f * 8 + s_tones[k]) * (Q + 1);
+        const float2 w = Wp[1], wq = Wp[Q];
         const float2* zp = s_z + (k + 1) * (Q + 1);  // = z_at(Mg - Mt + k Q): z[.. + j] at zp[j + j / Q]
-        float2 acc = make_float2(0.f, 0.f), wq = make_float2(1.f, 0.f);
+        float2 acc = make_float2(0.f, 0.f);
         for (int q = 0; q < Q; ++q) {
-          const float2 z = zp[q];
-          acc.x += z.x * wq.x - z.y * wq.y;
-          acc.y += z.x * wq.y + z.y * wq.x;
-          wq = make_float2(wq.x * w.x - wq.y * w.y, wq.x * w.y + wq.y * w.x);
+          const float2 z = zp[q], W = Wp[q];
+          acc.x = fmaf(z.x, W.x, fmaf(-z.y, W.y, acc.x));
+          acc.y = fmaf(z.x, W.y, fmaf(z.y, W.x, acc.y));
         }
 #pragma unroll
         for (int d = 0; d < kMaxT; ++d) {
@@ -618,8 +622,10 @@ hipError_t launch_sub_est(const SubLaunch& a, hipStream_t s) {
     // the rest launch: 8 workgroups per slot that exit at once unless the slot holds more than
     // kSubRecStride fits
     const unsigned grid_rest = (unsigned)(((a.n_slots + 7) / 8) * 8 * (int64_t)kSubRestStride);
-    // padded z rows -1 .. 81 and the decimation's twiddles (phases 2-3), then the pulse table (phase 4)
-    const size_t mz = (size_t)z_words(a.Q) + (size_t)(a.nsps / a.Q);
+    // padded z rows -1 .. 81, the decimation's twiddles and the fine sync's rotation powers (phases
+    // 2-3), then the pulse table (phase 4)
+    const int D = a.nsps / a.Q;
+    const size_t mz = (size_t)z_words(a.Q) + (size_t)((D + 1) & ~1) + (size_t)(2 * kMf + 1) * 8 * (a.Q + 1);
     const size_t lds = std::max(mz * sizeof(float2), (size_t)a.nsps * sizeof(float4));
     hipError_t e = hipSuccess;
     if (a.dtype == FT8_I16) {

@@ -1,0 +1,52 @@
+"""The reference's own sensitivity harness run here at two of its rates (build container only; imports
+/root/reference/src like tools/make_golden_harness.py): test_ft8_standard.py:43-68 test_step,
+`ROUNDS` rounds per SNR point, the reference's decode_ft8_message deciding success.  Inputs are
+seeded exactly as in make_golden_harness.py (np.random.default_rng(seed): payload, then noise; the
+clean wave from the reference generator), so the GPU test rebuilds the same float64 bytes and must
+reach the same per-slot verdicts (tests/test_gpu_harness.py::test_gpu_sensitivity_points_match_reference).
+
+This checks BASELINE.md section 1's table (snr_vs_freq_analysis.xlsx: -9 dB at B = 1 000 Hz, -13 dB at
+B = 3 000 Hz) against the committed harness and decoder: the success ratio per point is stored.
+
+Usage:  cd /tmp && python /root/repo/tools/make_golden_sensitivity.py
+"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import make_golden_harness as MH  # noqa: E402  (reference import recipe, harness_input, KW)
+
+POINTS = {2000: (-14.0, -13.0, -12.0, -11.0, -10.0), 6000: (-20.0, -19.0, -18.0, -17.0, -16.0, -15.0, -14.0)}
+ROUNDS = 20
+SEED0 = 70000
+
+
+def main():
+    import tempfile
+    os.chdir(tempfile.mkdtemp(prefix="ft8gold_"))
+    out = {"rounds": ROUNDS, "kwargs": MH.KW, "points": []}
+    seed = SEED0
+    for fs, snrs in POINTS.items():
+        for snr in snrs:
+            t0 = time.time()
+            seeds, ok = [], []
+            for _ in range(ROUNDS):
+                _p, _c, x = MH.harness_input(fs, snr, seed)
+                res = MH.quiet(MH.R.decode_ft8_message, x, fs, **MH.KW)
+                seeds.append(seed)
+                ok.append(len(res) > 0)
+                seed += 1
+            out["points"].append({"fs": fs, "snr_db": snr, "seeds": seeds, "success": ok,
+                                  "ratio": sum(ok) / ROUNDS})
+            print(fs, snr, sum(ok), "/", ROUNDS, round(time.time() - t0, 1), "s", flush=True)
+    with open(os.path.join(MH.GOLD, "sensitivity_ref.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    print("wrote", os.path.join(MH.GOLD, "sensitivity_ref.json"))
+
+
+if __name__ == "__main__":
+    main()
