@@ -104,3 +104,37 @@ def test_gpu_channel_fixture_drift_correction(gpu):
     y = np.asarray(y)
     assert y.shape == ref.shape and y.dtype == np.complex128
     assert np.max(np.abs(y - ref)) <= 1e-9 * np.max(np.abs(ref))
+
+
+def test_gpu_sensitivity_points_match_reference(gpu, oracle):
+    """The reference's own sensitivity harness (test_ft8_standard.py:43-123) at two of its rates,
+    run here with the reference deciding success (tools/make_golden_sensitivity.py ->
+    tests/golden/sensitivity_ref.json, 20 seeded rounds per SNR point): the GPU decodes the same
+    float64 inputs and reaches the same verdict on every slot -- so the GPU sweep's thresholds
+    (bench.py `sensitivity`) are the reference decoder's."""
+    import json
+    import os
+    import torch
+    from conftest import GOLD
+    from ft8_demodulator_amd import _lib
+    from ft8_demodulator_amd._pipeline import SlotDecoder
+    path = os.path.join(GOLD, "sensitivity_ref.json")
+    if not os.path.exists(path):
+        pytest.skip("tests/golden/sensitivity_ref.json not generated")
+    with open(path) as f:
+        ref = json.load(f)
+    kw = ref["kwargs"]
+    for pt in ref["points"]:
+        cases = [{"seed": s, "fs": pt["fs"], "snr_db": pt["snr_db"]} for s in pt["seeds"]]
+        xs = []
+        for c in cases:
+            rng = np.random.default_rng(c["seed"])
+            payload = rng.integers(0, 256, size=10, dtype=np.uint8)
+            clean = np.real(oracle.gfsk_waveform(oracle.tx_itones(bytes(payload)), c["fs"], 0.0, style=1))
+            noise = np.sqrt(np.mean(clean ** 2) / (10 ** (c["snr_db"] / 10))) * rng.standard_normal(len(clean))
+            xs.append(clean + noise)
+        dec = SlotDecoder(pt["fs"], kw["bins_per_tone"], kw["steps_per_symbol"], kw["max_candidates"],
+                          kw["min_score"], kw["max_iterations"])
+        recs = dec.records(torch.from_numpy(np.stack(xs)).cuda(), _lib.FT8_F64)
+        got = [len(r) > 0 for r in recs]
+        assert got == pt["success"], (pt["fs"], pt["snr_db"], got, pt["success"])
