@@ -9,3 +9,5 @@ timeout -k 10 300 python -u tools/experiments/sub_bench.py > gpurun_out/${T}_sub
 timeout -k 10 300 python -u tools/experiments/sub_bench.py > gpurun_out/${T}_sub_2.log 2>&1 &&
 bash tools/gpu_prof.sh ${T} &&
 bash tools/gpu_sub_prof.sh ${T}
+# then pass F's score-kernel variants (tools/gpu_r5f.sh)
+[ $? -eq 0 ] && bash tools/gpu_r5f.sh r5f
