@@ -237,7 +237,7 @@ __device__ __forceinline__ int pidx(int i) { return i + (i >> 4); }
 // One Stockham stage of radix R.  MAXV = max complex values per thread (P <= 256 * MAXV).
 // HALF (first stage only): inputs j + r nbf with r >= R / 2 are the frame's zero padding (real
 // input, nperseg <= P), set as constants so the butterfly's first layer folds away
-template <int R, int MAXV, bool FIRST, typename CT, typename Src, bool HALF = false>
+template <int R, int MAXV, bool FIRST, typename CT, typename Src, bool HALF = false, int TH = kThreads>
 __device__ __forceinline__ void stockham_stage(cplx<CT>* buf, int P, int Ns, const cplx<CT>* tw,
                                                const Src& src) {
   constexpr int MAXB = (MAXV + R - 1) / R;
@@ -246,7 +246,7 @@ __device__ __forceinline__ void stockham_stage(cplx<CT>* buf, int P, int Ns, con
   cplx<CT> v[MAXB][R];
 #pragma unroll
   for (int b = 0; b < MAXB; ++b) {
-    const int j = tid + b * kThreads;
+    const int j = tid + b * TH;
     if (j < nbf) {
 #pragma unroll
       for (int r = 0; r < R; ++r) {
@@ -260,7 +260,7 @@ __device__ __forceinline__ void stockham_stage(cplx<CT>* buf, int P, int Ns, con
   const int tstep = P / (Ns * R);
 #pragma unroll
   for (int b = 0; b < MAXB; ++b) {
-    const int j = tid + b * kThreads;
+    const int j = tid + b * TH;
     if (j < nbf) {
       const int k = j % Ns;
       if (!FIRST && k != 0) {
@@ -290,17 +290,17 @@ __device__ __forceinline__ void stockham_stage(cplx<CT>* buf, int P, int Ns, con
   __syncthreads();
 }
 
-template <int MAXV, bool FIRST, typename CT, typename Src>
+template <int MAXV, bool FIRST, int TH = kThreads, typename CT, typename Src>
 __device__ void run_stage(int R, cplx<CT>* buf, int P, int Ns, const cplx<CT>* tw, const Src& src) {
   switch (R) {
-    case 2: stockham_stage<2, MAXV, FIRST>(buf, P, Ns, tw, src); break;
-    case 3: stockham_stage<3, MAXV, FIRST>(buf, P, Ns, tw, src); break;
-    case 4: stockham_stage<4, MAXV, FIRST>(buf, P, Ns, tw, src); break;
-    case 5: stockham_stage<5, MAXV, FIRST>(buf, P, Ns, tw, src); break;
-    case 7: stockham_stage<7, MAXV, FIRST>(buf, P, Ns, tw, src); break;
-    case 15: stockham_stage<15, MAXV, FIRST>(buf, P, Ns, tw, src); break;
-    case 16: stockham_stage<16, MAXV, FIRST>(buf, P, Ns, tw, src); break;
-    default: stockham_stage<8, MAXV, FIRST>(buf, P, Ns, tw, src); break;
+    case 2: stockham_stage<2, MAXV, FIRST, CT, Src, false, TH>(buf, P, Ns, tw, src); break;
+    case 3: stockham_stage<3, MAXV, FIRST, CT, Src, false, TH>(buf, P, Ns, tw, src); break;
+    case 4: stockham_stage<4, MAXV, FIRST, CT, Src, false, TH>(buf, P, Ns, tw, src); break;
+    case 5: stockham_stage<5, MAXV, FIRST, CT, Src, false, TH>(buf, P, Ns, tw, src); break;
+    case 7: stockham_stage<7, MAXV, FIRST, CT, Src, false, TH>(buf, P, Ns, tw, src); break;
+    case 15: stockham_stage<15, MAXV, FIRST, CT, Src, false, TH>(buf, P, Ns, tw, src); break;
+    case 16: stockham_stage<16, MAXV, FIRST, CT, Src, false, TH>(buf, P, Ns, tw, src); break;
+    default: stockham_stage<8, MAXV, FIRST, CT, Src, false, TH>(buf, P, Ns, tw, src); break;
   }
 }
 
@@ -959,8 +959,10 @@ struct BlueArgs {
   const void* hspec;
 };
 
-template <typename InT, bool CPLX, typename CT, int MAXV>
-__global__ __launch_bounds__(kThreads, 1) void k_stft_blue(BlueArgs b) {
+// TH threads: 512 for P > 4096 (the float64 8192-point image is 139 KB: one workgroup per CU, so
+// 256 threads left 4 waves per CU through every stage's barriers)
+template <typename InT, bool CPLX, typename CT, int MAXV, int TH>
+__global__ __launch_bounds__(TH, 1) void k_stft_blue(BlueArgs b) {
   FT8_RACE_PROLOGUE();
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   cplx<CT>* buf = reinterpret_cast<cplx<CT>*>(smem);
@@ -982,22 +984,22 @@ __global__ __launch_bounds__(kThreads, 1) void k_stft_blue(BlueArgs b) {
   const int P = a.P;
   // forward FFT of a
   int Ns = 1;
-  run_stage<MAXV, true>(a.radix[0], buf, P, Ns, tw, src);
+  run_stage<MAXV, true, TH>(a.radix[0], buf, P, Ns, tw, src);
   Ns *= a.radix[0];
   for (int st = 1; st < a.nstages; ++st) {
-    run_stage<MAXV, false>(a.radix[st], buf, P, Ns, tw, src);
+    run_stage<MAXV, false, TH>(a.radix[st], buf, P, Ns, tw, src);
     Ns *= a.radix[st];
   }
   // times the block's filter spectrum, conjugated: the forward stages then give P conj(y)
   const cplx<CT>* H = reinterpret_cast<const cplx<CT>*>(b.hspec) + (int64_t)blk * P;
-  for (int k = threadIdx.x; k < P; k += kThreads) {
+  for (int k = threadIdx.x; k < P; k += TH) {
     const cplx<CT> y = cmul(buf[pidx(k)], H[k]);
     buf[pidx(k)] = {y.x, -y.y};
   }
   __syncthreads();
   Ns = 1;
   for (int st = 0; st < a.nstages; ++st) {
-    run_stage<MAXV, false>(a.radix[st], buf, P, Ns, tw, src);
+    run_stage<MAXV, false, TH>(a.radix[st], buf, P, Ns, tw, src);
     Ns *= a.radix[st];
   }
   // bins of this block inside the kept range -> dB row (argmax requests reduce the rows afterwards)
@@ -1005,7 +1007,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_stft_blue(BlueArgs b) {
   const int lo = max(k0, a.f_lo), hi = min(k0 + b.B, a.f_lo + a.nf_out);
   const CT inv = (CT)1 / (CT)P, scale = (CT)a.scale;
   CT* out = reinterpret_cast<CT*>(a.out) + ((int64_t)slot * a.nt_out + fi) * a.nf_out;
-  for (int k = lo + (int)threadIdx.x; k < hi; k += kThreads) {
+  for (int k = lo + (int)threadIdx.x; k < hi; k += TH) {
     const cplx<CT> v = buf[pidx(k - k0 + b.L - 1)];
     const cplx<CT> X = cmul(chirp[k], cplx<CT>{v.x * inv, -v.y * inv});
     const CT pw = (X.x * X.x + X.y * X.y) * scale;
@@ -1066,14 +1068,15 @@ hipError_t launch_blue(const StftLaunch& L, const StftArgs& a, hipStream_t s) {
   const int64_t units = (int64_t)a.nt_out * L.n_slots * b.nblk_run;
   b.s.per_xcd = (int)((units + 7) / 8);
   const size_t lds = (size_t)(a.P + a.P / 16 + 1) * sizeof(cplx<CT>);
-  if (a.P > kThreads * 32 || L.plan.L > a.P) return hipErrorInvalidValue;
-  auto kern = a.P <= kThreads * 16 ? k_stft_blue<InT, CPLX, CT, 16> : k_stft_blue<InT, CPLX, CT, 32>;
+  if (a.P > 512 * 16 || L.plan.L > a.P) return hipErrorInvalidValue;
+  const bool wide = a.P > kThreads * 16;
+  auto kern = !wide ? k_stft_blue<InT, CPLX, CT, 16, kThreads> : k_stft_blue<InT, CPLX, CT, 16, 512>;
   if (lds > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)lds);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(kern, dim3((unsigned)(8 * b.s.per_xcd)), dim3(kThreads), lds, s, b);
+  hipLaunchKernelGGL(kern, dim3((unsigned)(8 * b.s.per_xcd)), dim3(wide ? 512 : kThreads), lds, s, b);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || !L.argmax) return e;
   const int64_t rows = (int64_t)a.nt_out * L.n_slots;
