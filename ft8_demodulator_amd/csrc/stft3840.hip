@@ -518,8 +518,9 @@ __device__ __forceinline__ void pk_stages(f2* buf, const f2* tw) {
   if constexpr (sizeof...(Rest) > 0) pk_stages<TH, P, NS * R, Rest...>(buf, tw);
 }
 
-// TH threads per frame: 256, or 512 for the 9 600-point plan, whose 82 KB image allows only two
-// workgroups per CU (8 resident waves at 256 threads: the barriers between stages left the SIMDs idle)
+// TH threads per frame: 256, or 640 for the 9 600-point plan, whose 82 KB image allows only two
+// workgroups per CU (8 resident waves at 256 threads: the barriers between stages left the SIMDs
+// idle); its stages' 600 / 1 200 / 640 / 1 920 butterflies fill 640 lanes to 94-100 %
 template <typename InT, int TH, int P, int... Rs>
 __global__ __launch_bounds__(TH) void k_stft_pk(PkArgs a) {
   FT8_RACE_PROLOGUE();
@@ -628,7 +629,7 @@ hipError_t launch_stft3840(const StftLaunch& L, hipStream_t s) {
 struct PkPlan {
   int P, n, r[4];
 };
-constexpr int kPk9600Threads = 512;
+constexpr int kPk9600Threads = 640;
 constexpr PkPlan kPkPlans[] = {{3200, 4, {16, 8, 5, 5}}, {9600, 4, {16, 8, 15, 5}}, {960, 3, {16, 4, 15}}};
 
 static int pk_plan_of(const StftLaunch& L) {
