@@ -466,13 +466,12 @@ struct PkArgs {
 
 // one Stockham stage (not the first): butterfly j = t + TH b of nbf = P / R, Ns = NS
 template <int TH, int P, int NS, int R>
-__device__ __forceinline__ void pk_stage(f2* buf, const f2* tw) {
+__device__ __forceinline__ void pk_stage(f2* buf, const f2* tw, const int t) {
   constexpr int NBF = P / R, NB = (NBF + TH - 1) / TH, TSTEP = P / (NS * R);
   // every index step is a multiple of 16, so pidx(x + 16 m) = pidx(x) + 17 m: one address per
   // butterfly and immediates (as k_stft3840p)
   static_assert(NBF % 16 == 0 && NS % 16 == 0, "linear padded index steps");
   constexpr int RSTEP = NBF + NBF / 16, WSTEP = NS + NS / 16;
-  const int t = threadIdx.x;
   f2 v[NB][R];
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
@@ -513,42 +512,86 @@ __device__ __forceinline__ void pk_stage(f2* buf, const f2* tw) {
 }
 
 template <int TH, int P, int NS, int R, int... Rest>
-__device__ __forceinline__ void pk_stages(f2* buf, const f2* tw) {
-  pk_stage<TH, P, NS, R>(buf, tw);
-  if constexpr (sizeof...(Rest) > 0) pk_stages<TH, P, NS * R, Rest...>(buf, tw);
+__device__ __forceinline__ void pk_stages(f2* buf, const f2* tw, const int t) {
+  pk_stage<TH, P, NS, R>(buf, tw, t);
+  if constexpr (sizeof...(Rest) > 0) pk_stages<TH, P, NS * R, Rest...>(buf, tw, t);
 }
 
 // TH threads per frame: 256, or 640 for the 9 600-point plan, whose 82 KB image allows only two
 // workgroups per CU (8 resident waves at 256 threads: the barriers between stages left the SIMDs
-// idle); its stages' 600 / 1 200 / 640 / 1 920 butterflies fill 640 lanes to 94-100 %
-template <typename InT, int TH, int P, int... Rs>
+// idle); its stages' 600 / 1 200 / 640 / 1 920 butterflies fill 640 lanes to 94-100 %.
+// A workgroup transforms FR consecutive frames of one slot in turn (round 5; the 3 200- and
+// 960-point plans two, the 9 600-point one one): the window pairs its stage-1 inputs take are the
+// same in every frame and stay in registers, and the frame's loads carry no per-lane branch.  One
+// frame per workgroup had the 20 kHz plan's waves 73 % of their time in waits (its loads, each in
+// its own branch, at the head of every frame).  Measured (profiles/r5_{j,k,m,p}_geo_*): 20 kHz STFT
+// 0.54-0.56 ms -> 0.455-0.475 at FR 2 (FR 3 / 4 / 6 / 8: 0.45 / 0.46 / 0.46 / 0.48-0.51; the next
+// frame prefetched into registers: 0.51); the 9 600-point plan keeps one frame (0.85-1.20 ms at any
+// FR > 1, where the loop-invariant stage addresses stay live: up to 144 VGPRs).
+constexpr int kPkFrames = 2;
+template <typename InT, int TH, int FR, int P, int... Rs>
 __global__ __launch_bounds__(TH) void k_stft_pk(PkArgs a) {
   FT8_RACE_PROLOGUE();
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_pk[];
   f2* buf = reinterpret_cast<f2*>(smem_pk);
   const int t = threadIdx.x;
   const int nt = a.nt_out;
+  const int chunks = (nt + FR - 1) / FR;
   const int rr = (int)(blockIdx.x & 7) * a.per_xcd + (int)(blockIdx.x >> 3);  // XCD-aware, as k_stft
-  if (rr >= nt * a.n_slots) return;
-  const int slot = rr / nt;
-  const int fi = rr - slot * nt;
-  const InT* xs = reinterpret_cast<const InT*>(a.samples) + (int64_t)slot * a.slot_stride + (int64_t)(a.t_lo + fi) * a.hop;
+  if (rr >= chunks * a.n_slots) return;
+  const int slot = rr / chunks;
+  const int f_begin = (rr - slot * chunks) * FR, f_end = min(nt, f_begin + FR);
   // stage 1: radix 16, Ns = 1, over the frame's nonzero half: inputs z[j + r P / 16], r < 8, with
   // z[n] = (w[2n] x[2n], w[2n+1] x[2n+1]) (zero past nperseg) -> buf[16 j + k]
-  {
-    constexpr int NBF = P / 16, NB = (NBF + TH - 1) / TH;
+  constexpr int NBF = P / 16, NB = (NBF + TH - 1) / TH;
+  // FR > 1: a stage-1 operand is the pair at min(n0, nperseg - 2) (in bounds for every lane), then a
+  // select: the pair itself, (x[n0], 0) at n0 = nperseg - 1, or zero
+  auto pick = [&](int n0, f2 p) {
+    return n0 + 1 < a.nperseg ? p : f2{n0 < a.nperseg ? p.y : 0.0f, 0.0f};
+  };
+  auto window_pair = [&](int n0) {
+    return pick(n0, *reinterpret_cast<const f2*>(a.window + min(n0, a.nperseg - 2)));
+  };
+  f2 wz[NB][8];
+  if constexpr (FR > 1) {
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+#pragma unroll
+      for (int r = 0; r < 8; ++r) wz[b][r] = t + TH * b < NBF ? window_pair(2 * (t + TH * b + r * NBF)) : f2{0.0f, 0.0f};
+    }
+  }
+  const InT* xslot = reinterpret_cast<const InT*>(a.samples) + (int64_t)slot * a.slot_stride;
+  constexpr float kDb = 3.0102999566398119521f;  // 10 log10(v) = (10 log10 2) log2(v), v >= 1e-12
+  const float qscale = 0.25f * a.scale;          // |2 X|^2 / 4 / (sum w)^2
+#pragma unroll 1
+  for (int fi = f_begin; fi < f_end; ++fi) {
+    if (fi > f_begin) __syncthreads();  // the previous frame's epilogue has read the image
+    const InT* xs = xslot + (int64_t)(a.t_lo + fi) * a.hop;
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
       const int j = t + TH * b;
       if (j < NBF) {
         f2 z[8], y[16];
+        if constexpr (FR > 1) {
+          // every lane loads (the pair at min(n0, nperseg - 2), in bounds) and selects, so a frame's
+          // loads issue together: a load inside a per-lane branch waited for each in turn
 #pragma unroll
-        for (int r = 0; r < 8; ++r) {
-          const int n0 = 2 * (j + r * NBF);
-          if (n0 + 1 < a.nperseg) {
-            z[r] = *reinterpret_cast<const f2*>(a.window + n0) * load_pair<InT>(xs, n0);
-          } else {
-            z[r] = f2{n0 < a.nperseg ? a.window[n0] * load_pair<InT>(xs, n0).x : 0.0f, 0.0f};
+          for (int r = 0; r < 8; ++r) {
+            const int n0 = 2 * (j + r * NBF);
+            z[r] = wz[b][r] * pick(n0, load_pair<InT>(xs, min(n0, a.nperseg - 2)));
+          }
+        } else {
+          // one frame per workgroup (the 9 600-point plan: its 1 920-sample window covers a fifth of
+          // the transformed half):
+          // per-lane branches, so the zero part's loads are skipped
+#pragma unroll
+          for (int r = 0; r < 8; ++r) {
+            const int n0 = 2 * (j + r * NBF);
+            if (n0 + 1 < a.nperseg) {
+              z[r] = *reinterpret_cast<const f2*>(a.window + n0) * load_pair<InT>(xs, n0);
+            } else {
+              z[r] = f2{n0 < a.nperseg ? a.window[n0] * load_pair<InT>(xs, n0).x : 0.0f, 0.0f};
+            }
           }
         }
         dft16_half(z, y);
@@ -557,37 +600,42 @@ __global__ __launch_bounds__(TH) void k_stft_pk(PkArgs a) {
       }
     }
     __syncthreads();
-  }
-  pk_stages<TH, P, 16, Rs...>(buf, a.tw);
-  // epilogue: X[k] = (s - i W_2P^k d) / 2, s = Z[k] + conj Z[P-k], d = Z[k] - conj Z[P-k]
-  constexpr float kDb = 3.0102999566398119521f;  // 10 log10(v) = (10 log10 2) log2(v), v >= 1e-12
-  const float qscale = 0.25f * a.scale;          // |2 X|^2 / 4 / (sum w)^2
-  float* out = a.out + ((int64_t)slot * nt + fi) * a.nf_out;
-  if (a.f_lo == 0 && a.nf_out == P) {
-    // every f >= 0 bin kept: bins k and P - k share s and d (k_stft3840p's full-band epilogue):
-    // one pair of LDS reads, one post-twiddle and one packed power for both
-    for (int k = t; k <= P / 2; k += TH) {
-      const f2 A = lds_ld(&buf[pidx(k)]);
-      const f2 B = lds_ld(&buf[pidx(k == 0 ? 0 : P - k)]);
-      const f2 sm = add_cj(A, B), df = sub_cj(A, B);
-      const f2 wd = cmul(a.post[k], df);
-      const f2 re = re_pm(sm, wd), im = im_mp(sm, wd);  // (X1.x, X2.x), (X1.y, -X2.y)
-      const f2 pp = (re * re + im * im) * splat(qscale) + splat(1e-12f);
-      out[k] = kDb * __builtin_amdgcn_logf(pp.x);
-      if (k != 0 && k != P / 2) out[P - k] = kDb * __builtin_amdgcn_logf(pp.y);
+    // re-opaque the thread index and the tables' addresses each frame, so the stages' LDS
+    // addresses and twiddle loads (the same in every frame) are recomputed, not hoisted out of the
+    // loop into ~90 live registers
+    const f2* tw = a.tw;
+    const f2* post = a.post;
+    int tf = t;
+    if constexpr (FR > 1) asm volatile("" : "+s"(tw), "+s"(post), "+v"(tf));
+    pk_stages<TH, P, 16, Rs...>(buf, tw, tf);
+    // epilogue: X[k] = (s - i W_2P^k d) / 2, s = Z[k] + conj Z[P-k], d = Z[k] - conj Z[P-k]
+    float* out = a.out + ((int64_t)slot * nt + fi) * a.nf_out;
+    if (a.f_lo == 0 && a.nf_out == P) {
+      // every f >= 0 bin kept: bins k and P - k share s and d (k_stft3840p's full-band epilogue):
+      // one pair of LDS reads, one post-twiddle and one packed power for both
+      for (int k = t; k <= P / 2; k += TH) {
+        const f2 A = lds_ld(&buf[pidx(k)]);
+        const f2 B = lds_ld(&buf[pidx(k == 0 ? 0 : P - k)]);
+        const f2 sm = add_cj(A, B), df = sub_cj(A, B);
+        const f2 wd = cmul(post[k], df);
+        const f2 re = re_pm(sm, wd), im = im_mp(sm, wd);  // (X1.x, X2.x), (X1.y, -X2.y)
+        const f2 pp = (re * re + im * im) * splat(qscale) + splat(1e-12f);
+        out[k] = kDb * __builtin_amdgcn_logf(pp.x);
+        if (k != 0 && k != P / 2) out[P - k] = kDb * __builtin_amdgcn_logf(pp.y);
+      }
+      continue;
     }
-    return;
-  }
-  for (int i = t; i < a.nf_out; i += TH) {
-    const int k = a.f_lo + i;
-    const int kk = (k <= P) ? k : 2 * P - k;  // real signal: X[N-k] = conj X[k]
-    const f2 A = lds_ld(&buf[pidx(kk == P ? 0 : kk)]);
-    const f2 B = lds_ld(&buf[pidx(kk == 0 ? 0 : P - kk)]);
-    const f2 sm = add_cj(A, B), df = sub_cj(A, B);
-    const f2 wd = cmul(a.post[kk], df);
-    const f2 X = add_mi(sm, wd);
-    const f2 qq = X * X;
-    out[i] = kDb * __builtin_amdgcn_logf((qq.x + qq.y) * qscale + 1e-12f);
+    for (int i = t; i < a.nf_out; i += TH) {
+      const int k = a.f_lo + i;
+      const int kk = (k <= P) ? k : 2 * P - k;  // real signal: X[N-k] = conj X[k]
+      const f2 A = lds_ld(&buf[pidx(kk == P ? 0 : kk)]);
+      const f2 B = lds_ld(&buf[pidx(kk == 0 ? 0 : P - kk)]);
+      const f2 sm = add_cj(A, B), df = sub_cj(A, B);
+      const f2 wd = cmul(post[kk], df);
+      const f2 X = add_mi(sm, wd);
+      const f2 qq = X * X;
+      out[i] = kDb * __builtin_amdgcn_logf((qq.x + qq.y) * qscale + 1e-12f);
+    }
   }
 }
 
@@ -665,7 +713,9 @@ hipError_t launch_stftpk(const StftLaunch& L, hipStream_t s) {
   if (a.nt_out <= 0 || a.nf_out <= 0 || L.n_slots <= 0) return hipSuccess;
   const int q = pk_plan_of(L);
   if (q < 0) return hipErrorInvalidValue;
-  a.per_xcd = (int)(((int64_t)a.nt_out * L.n_slots + 7) / 8);
+  // frames per workgroup (FR of the instantiation below)
+  const int fr = q == 1 ? 1 : kPkFrames;
+  a.per_xcd = (int)(((int64_t)((a.nt_out + fr - 1) / fr) * L.n_slots + 7) / 8);
   const dim3 grid((unsigned)(8 * a.per_xcd));
   const size_t lds = (size_t)(kPkPlans[q].P + kPkPlans[q].P / 16 + 1) * sizeof(f2);
   auto go = [&](auto kern) {
@@ -678,11 +728,15 @@ hipError_t launch_stftpk(const StftLaunch& L, hipStream_t s) {
   };
   const bool i16 = L.dtype == FT8_I16;
   switch (q) {
-    case 0: return i16 ? go(k_stft_pk<int16_t, kThreads38, 3200, 8, 5, 5>) : go(k_stft_pk<float, kThreads38, 3200, 8, 5, 5>);
+    case 0:
+      return i16 ? go(k_stft_pk<int16_t, kThreads38, kPkFrames, 3200, 8, 5, 5>)
+                 : go(k_stft_pk<float, kThreads38, kPkFrames, 3200, 8, 5, 5>);
     case 1:
-      return i16 ? go(k_stft_pk<int16_t, kPk9600Threads, 9600, 8, 15, 5>)
-                 : go(k_stft_pk<float, kPk9600Threads, 9600, 8, 15, 5>);
-    default: return i16 ? go(k_stft_pk<int16_t, kThreads38, 960, 4, 15>) : go(k_stft_pk<float, kThreads38, 960, 4, 15>);
+      return i16 ? go(k_stft_pk<int16_t, kPk9600Threads, 1, 9600, 8, 15, 5>)
+                 : go(k_stft_pk<float, kPk9600Threads, 1, 9600, 8, 15, 5>);
+    default:
+      return i16 ? go(k_stft_pk<int16_t, kThreads38, kPkFrames, 960, 4, 15>)
+                 : go(k_stft_pk<float, kThreads38, kPkFrames, 960, 4, 15>);
   }
 }
 
