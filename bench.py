@@ -5,7 +5,9 @@ One step = one ft8_decode_batch over a batch of 256 independent synthetic 15-s s
 20 BP iterations): STFT -> Costas sync -> selection -> LLR -> BP -> CRC, samples already
 resident in HBM.  With N > 1 GPUs each rank decodes its own 256 slots (weak scaling) and the
 step ends with an RCCL all-gather of every rank's decodes, packed on the device (the path's one
-exchange; no host sync inside the step).
+exchange; no host sync inside the step).  Consecutive steps alternate over --depth (default 2)
+decoders, each with its own context and stream, so one step's front end overlaps the previous
+step's k_bp tail; every step decodes the whole batch (`depth.one_chain`: the same steps as one chain).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--slots S] [--no-cpu] [--gather]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -17,6 +19,8 @@ Rank r decodes global slots [256 r, 256 (r + 1)) (per-slot seeds 100000 + slot),
 is the first shard of every larger run.
 
 Prints ONE JSON line on rank 0.  Besides the contract fields it carries:
+  depth         contexts / streams the timed steps alternate over; one_chain: the same K steps on one
+                context and one stream, timed after the loop (N=1)
   roofline      the dominant kernel (k_bp: LLR + float64 BP + CRC), FLOP-rate vs the FP64 vector peak
   roofline_hbm  the HBM-bound STFT kernel, GB/s vs the 8 TB/s HBM peak
   stages_ms     per-kernel device time per step (HIP events on the decode stream)
@@ -1009,6 +1013,10 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--slots", type=int, default=256, help="slots per GPU per step")
+    ap.add_argument("--depth", type=int, default=2,
+                    help="consecutive steps alternate over this many contexts, each on its own stream, so one "
+                         "step's STFT / sync can start while the previous step's k_bp retires its last waves "
+                         "(1: one chain on one stream)")
     ap.add_argument("--signals", type=int, default=50)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-slots", type=int, default=256)
@@ -1106,8 +1114,17 @@ def main():
     torch.cuda.synchronize()
     dec = SlotDecoder(12000, 2, 2, device=dev, **kw)
     ctx = dec.ctx
-    ctx.set_timing(True)   # allocates the device BP work counters; no events in the timed loop
-    ctx.set_timing(False)
+    # --depth D: step k runs on decoder k % D -- its own context (scratch, BP claim counters) and its
+    # own stream -- so consecutive steps overlap only where the hardware lets them (the next step's
+    # front end filling the CUs k_bp's last waves leave); every step still decodes the whole batch
+    D = max(1, args.depth)
+    decs = [dec] + [SlotDecoder(12000, 2, 2, device=dev, **kw) for _ in range(D - 1)]
+    for d_ in decs[1:]:
+        d_.ctx = _lib.Context(local)
+    streams = [torch.cuda.current_stream(dev)] if D == 1 else [torch.cuda.Stream(dev) for _ in range(D)]
+    for d_ in decs:
+        d_.ctx.set_timing(True)   # allocates the device BP work counters; no events in the timed loop
+        d_.ctx.set_timing(False)
 
     # N > 1 (or --gather): every step ends with the decode exchange -- ft8_pack_decodes on the device,
     # one all-gather of the packed buffer, no host sync (distributed.DecodeGatherer); the last
@@ -1116,33 +1133,48 @@ def main():
     gatherer = DecodeGatherer(S, dec.cap, slot_offset=rank * S) if exchange else None
     handles = []
 
-    def step(keep=False):
-        out, counts = dec.run(x)
-        if exchange:
-            h = gatherer.start(out, counts)
-            if keep:
-                handles.append(h)   # every timed step's exchange is resolved after the loop
+    def step(k, keep=False, ev=None):
+        with torch.cuda.stream(streams[k % D]):
+            out, counts = decs[k % D].run(x)
+            if exchange:
+                h = gatherer.start(out, counts)
+                if keep:
+                    handles.append(h)   # every timed step's exchange is resolved after the loop
+            if ev is not None:
+                ev.record()             # on this step's stream, after its work
         return counts
 
-    for _ in range(args.warmup):
-        step()
+    for k_ in range(max(args.warmup, D)):
+        step(k_)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    # one HIP event after every timed step (recorded on the stream, no host sync): the per-step GPU
-    # periods show whether the timed steps had settled (k_bp's clock ramps over its first launches)
+    # one HIP event after every timed step (recorded on the step's stream, no host sync): the
+    # per-step GPU periods show whether the timed steps had settled (k_bp's clock ramps over its
+    # first launches); with D > 1 a period is the spacing of consecutive steps' completions
     step_ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     t0 = time.perf_counter()
     step_ev[0].record()
     for i_ in range(args.steps):
-        counts = step(keep=True)
-        step_ev[i_ + 1].record()
+        counts = step(i_, keep=True, ev=step_ev[i_ + 1])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     step_ms = [step_ev[i_].elapsed_time(step_ev[i_ + 1]) for i_ in range(args.steps)]
+    # the same K steps as one chain (D = 1) right after, on the first decoder and the default
+    # stream: what the overlap of consecutive steps is worth on this box
+    depth1 = None
+    if D > 1 and world == 1:
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            dec.run(x)
+        torch.cuda.synchronize()
+        dt1 = (time.perf_counter() - t1) / args.steps
+        depth1 = {"ms_per_step": dt1 * 1e3, "value": S / dt1,
+                  "what": "the same steps on one context and one stream, timed after the line's loop"}
     decoded = int(counts.sum().item())
     gather = None
     gather_last = None
@@ -1175,7 +1207,7 @@ def main():
             ctx.bp_clock(reset=True)
         ctx.set_timing(True, stages=[st])
         for _ in range(R):
-            step()
+            step(0)   # the first decoder (this context), one chain
         torch.cuda.synchronize()
         ctx.set_timing(False)
         tm = ctx.timing(reset=True)[st]
@@ -1336,6 +1368,7 @@ def main():
                                "K=300 candidates, min_score=2, 20 BP iterations (config 5 shape at N>1)",
                    "slots_per_gpu": S, "sample_rate": 12000, "samples_per_slot": int(x.shape[1]),
                    "max_candidates": 300, "min_score": 2, "max_iterations": 20,
+                   "pipeline_depth": D,
                    "parallelism": f"slot-sharded x{world}" + (
                        (", one all-gather per step of the device-packed decodes over "
                         + ("gloo (--share-gpu rehearsal, every rank on cuda:0)" if args.share_gpu else "RCCL")
@@ -1351,6 +1384,7 @@ def main():
                      "bp_passes_per_launch": cn["passes"] / R, "candidates_per_launch": cn["candidates"] / R,
                      "clock": bp_clock, "issue": issue},
         "step_times": step_times,
+        "depth": {"contexts": D, "streams": D if D > 1 else 1, "one_chain": depth1},
         "step_hbm": {"what": "BASELINE.md whole-step accounting: slots/s per GPU x B_slot algorithmic bytes "
                              "(the step is FP64-VALU bound in k_bp, so this fraction is low by construction)",
                      "bytes_per_slot": b_slot, "achieved": step_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",

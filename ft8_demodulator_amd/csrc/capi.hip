@@ -89,6 +89,11 @@ struct ft8_ctx {
   // the kernels of the last single-chain ft8_decode_batch, for ft8_replay_stage (benchmarking):
   // valid until the next entry point that may reallocate the context's scratch
   bool replay_ok = false;
+  // the stream of the last entry point that enqueued work, and an event recorded on it after that
+  // work (StreamOrder): a call on another stream first waits for it
+  hipStream_t last_stream = nullptr;
+  hipEvent_t last_done = nullptr;
+  bool have_last = false;
   StftLaunch last_stft{};
   SyncLaunch last_sync{};
   BpLaunch last_bp{};
@@ -191,6 +196,35 @@ struct StageTimer {
       (void)hipEventRecord(b, s);
       c->pending.push_back({stage, a, b});
       a = nullptr;
+    }
+  }
+};
+
+// Stream order of a context's work.  The scratch buffers, the k_bp claim counters and their
+// host-side ticket bases assume that a context's launches run one after another; an entry point
+// that uses them, called on a stream other than the previous such call's, first waits (device side,
+// no host sync) for an event recorded after that call's work.  (Entry points that touch no context
+// state -- ft8_sync_score, ft8_llr, ft8_normalize, ft8_encode, ft8_pack_decodes, ft8_crc14,
+// ft8_ldpc_check -- take no part, so they never serialise two contexts' streams.)  Without it, two streams sharing one context (e.g. one
+// host thread alternating torch streams) would run two calls' kernels concurrently on the same
+// scratch and interleave the tickets of two k_bp launches.
+struct StreamOrder {
+  ft8_ctx* c;
+  hipStream_t s;
+  StreamOrder(ft8_ctx* c_, hipStream_t s_) : c(c_), s(s_) {
+    if (!c) return;
+    if (c->have_last && c->last_stream != s) (void)hipStreamWaitEvent(s, c->last_done, 0);
+  }
+  ~StreamOrder() {
+    if (!c) return;
+    DeviceGuard dg(c->device);  // the event lives on the context's device
+    if (!c->last_done && hipEventCreateWithFlags(&c->last_done, hipEventDisableTiming) != hipSuccess) {
+      c->last_done = nullptr;
+      return;
+    }
+    if (hipEventRecord(c->last_done, s) == hipSuccess) {
+      c->last_stream = s;
+      c->have_last = true;
     }
   }
 };
@@ -1028,6 +1062,7 @@ int ft8_destroy(ft8_ctx* c) {
     for (auto st : c->streams) (void)hipStreamDestroy(st);
     for (auto ev : c->joins) (void)hipEventDestroy(ev);
     if (c->fork) (void)hipEventDestroy(c->fork);
+    if (c->last_done) (void)hipEventDestroy(c->last_done);
   }
   delete c;
   return FT8_OK;
@@ -1050,6 +1085,7 @@ int ft8_geometry(int32_t fs, int32_t bpt, int32_t sps, int64_t n, int32_t* npers
 
 int ft8_stft(ft8_ctx* c, const void* d_samples, int dtype, int64_t n_samples, int32_t n_slots, int64_t slot_stride,
              const ft8_params* p, void* d_wf, void* stream) {
+  StreamOrder order_(c, (hipStream_t)stream);
   if (c) c->replay_ok = false;
   if (!c || !p || (!d_samples && n_slots > 0) || (!d_wf && n_slots > 0)) return fail(c, FT8_E_ARG, "null argument");
   DeviceGuard dg(c->device);
@@ -1093,6 +1129,7 @@ int ft8_stft_method(ft8_ctx* c, int32_t fs, int32_t bpt, int32_t sps, int64_t n,
 int ft8_sync_select(ft8_ctx* c, const void* d_wf, int wf_f64, int32_t n_slots, int32_t T, int32_t F,
                     const ft8_params* p, int32_t* d_cand, double* d_cand_score, int32_t* d_cand_count,
                     void* d_scores, void* stream) {
+  StreamOrder order_(c, (hipStream_t)stream);
   if (c) c->replay_ok = false;
   if (!c || !p || !d_cand_count) return fail(c, FT8_E_ARG, "null argument");
   if (T < 0 || F < 0 || n_slots < 0) return fail(c, FT8_E_ARG, "negative size");
@@ -1154,6 +1191,7 @@ int ft8_normalize(ft8_ctx* c, const double* d_in, int32_t n, double* d_out, void
 
 int ft8_bp(ft8_ctx* c, const double* d_llr, int32_t n, int32_t max_iterations, uint8_t* d_plain, ft8_result* d_res,
            void* stream) {
+  StreamOrder order_(c, (hipStream_t)stream);
   if (c) c->replay_ok = false;
   if (!c || (!d_llr && n > 0)) return fail(c, FT8_E_ARG, "bad argument");
   if (n <= 0) return FT8_OK;
@@ -1181,6 +1219,7 @@ int ft8_bp(ft8_ctx* c, const double* d_llr, int32_t n, int32_t max_iterations, u
 int ft8_decode_batch(ft8_ctx* c, const void* d_samples, int dtype, int64_t n_samples, int32_t n_slots,
                      int64_t slot_stride, const ft8_params* p, ft8_result* d_out, int32_t* d_counts,
                      int32_t cap, void* stream) {
+  StreamOrder order_(c, (hipStream_t)stream);
   if (c) c->replay_ok = false;
   if (!c || !p || !d_counts || (n_slots > 0 && !d_samples) || n_slots < 0 || cap < 0)
     return fail(c, FT8_E_ARG, "bad argument");
@@ -1265,6 +1304,7 @@ int ft8_encode(ft8_ctx* c, const uint8_t* d_msg, int32_t msg_bytes, int32_t n, u
 int ft8_synthesize(ft8_ctx* c, const uint8_t* d_tones, const ft8_tx_signal* d_signals, int32_t n_signals,
                    int32_t sample_rate, int32_t style, void* d_out, int out_dtype, int64_t n_samples, int32_t n_slots,
                    int64_t slot_stride, void* stream) {
+  StreamOrder order_(c, (hipStream_t)stream);
   if (c) c->replay_ok = false;
   if (!c || n_signals < 0 || n_slots < 0 || n_samples < 0 || sample_rate <= 0) return fail(c, FT8_E_ARG, "bad argument");
   if (style != FT8_TX_PROTOCOL && style != FT8_TX_REFERENCE) return fail(c, FT8_E_ARG, "unknown ft8_tx_style");
@@ -1298,6 +1338,7 @@ int ft8_synthesize(ft8_ctx* c, const uint8_t* d_tones, const ft8_tx_signal* d_si
 int ft8_subtract(ft8_ctx* c, const void* d_samples, int dtype, float* d_residual, int64_t n_samples, int32_t n_slots,
                  int64_t slot_stride, const ft8_params* p, const ft8_result* d_res, const int32_t* d_counts, int32_t cap,
                  void* stream) {
+  StreamOrder order_(c, (hipStream_t)stream);
   if (c) c->replay_ok = false;
   if (!c || !p || n_slots < 0 || cap < 0 || n_samples < 0) return fail(c, FT8_E_ARG, "bad argument");
   if (n_slots == 0 || n_samples == 0) {
@@ -1314,6 +1355,7 @@ int ft8_subtract(ft8_ctx* c, const void* d_samples, int dtype, float* d_residual
 }
 
 int ft8_subtract_fits(ft8_ctx* c, ft8_sub_fit* d_out, int32_t n_slots, int32_t cap, void* stream) {
+  StreamOrder order_(c, (hipStream_t)stream);
   if (!c || (!d_out && n_slots > 0 && cap > 0)) return fail(c, FT8_E_ARG, "bad argument");
   if (n_slots != c->sub_slots || cap != c->sub_cap)
     return fail(c, FT8_E_ARG, "n_slots / cap differ from the last subtraction's (" + std::to_string(c->sub_slots) +
@@ -1328,6 +1370,7 @@ int ft8_subtract_fits(ft8_ctx* c, ft8_sub_fit* d_out, int32_t n_slots, int32_t c
 
 int ft8_stft_argmax(ft8_ctx* c, const void* d_samples, int dtype, int64_t n_samples, int32_t n_slots,
                     int64_t slot_stride, const ft8_params* p, int32_t* d_idx, void* stream) {
+  StreamOrder order_(c, (hipStream_t)stream);
   if (c) c->replay_ok = false;
   if (!c || !p || (n_slots > 0 && (!d_samples || !d_idx))) return fail(c, FT8_E_ARG, "null argument");
   if (n_slots < 0 || n_samples < 0) return fail(c, FT8_E_ARG, "negative size");
@@ -1339,6 +1382,7 @@ int ft8_stft_argmax(ft8_ctx* c, const void* d_samples, int dtype, int64_t n_samp
 int ft8_drift_fit(ft8_ctx* c, int32_t stage, const int32_t* d_idx, int32_t n_slots, int32_t T, int32_t F,
                   const ft8_drift_params* p, ft8_drift_result* d_res, double* d_metric, int32_t* d_segments,
                   int32_t max_segments, void* stream) {
+  StreamOrder order_(c, (hipStream_t)stream);
   if (c) c->replay_ok = false;
   if (!c || !p) return fail(c, FT8_E_ARG, "null argument");
   if (stage != 1 && stage != 2) return fail(c, FT8_E_ARG, "stage must be 1 or 2");
@@ -1353,6 +1397,7 @@ int ft8_drift_fit(ft8_ctx* c, int32_t stage, const int32_t* d_idx, int32_t n_slo
 int ft8_drift_correct(ft8_ctx* c, const void* d_samples, int dtype, int64_t n_samples, int32_t n_slots,
                       int64_t slot_stride, const ft8_drift_params* p, void* d_out, ft8_drift_result* d_res,
                       void* stream) {
+  StreamOrder order_(c, (hipStream_t)stream);
   if (c) c->replay_ok = false;
   if (!c || !p) return fail(c, FT8_E_ARG, "null argument");
   if (n_slots < 0 || n_samples < 0) return fail(c, FT8_E_ARG, "negative size");
@@ -1414,6 +1459,7 @@ const char* ft8_build_id(void) { return FT8_BUILD_ID; }
 const char* ft8_build_flags(void) { return FT8_BUILD_FLAGS; }
 
 int ft8_replay_stage(ft8_ctx* c, int32_t stage, int32_t reps, void* stream) {
+  StreamOrder order_(c, (hipStream_t)stream);
   if (!c || reps < 0) return fail(c, FT8_E_ARG, "bad argument");
   if (!c->replay_ok) return fail(c, FT8_E_ARG, "no single-chain ft8_decode_batch to replay");
   DeviceGuard dg(c->device);
@@ -1461,6 +1507,7 @@ int ft8_pack_decodes(ft8_ctx* c, const ft8_result* d_records, const int32_t* d_c
 }
 
 int ft8_select_warnings(ft8_ctx* c, int32_t* d_out, int32_t n_slots, void* stream) {
+  StreamOrder order_(c, (hipStream_t)stream);
   if (!c || !d_out || n_slots < 0) return fail(c, FT8_E_ARG, "bad argument");
   if (n_slots == 0) return FT8_OK;
   if (!c->warn.p || c->warn.cap < sizeof(int32_t) * n_slots) return fail(c, FT8_E_ARG, "no selection has run");

@@ -14,7 +14,10 @@
  *     stream).  Results are valid after the stream is synchronised.
  *   - Return 0 (FT8_OK) on success, a negative FT8_E_* code otherwise; ft8_last_error() gives the
  *     message.  No C++ exception crosses this boundary.
- *   - One context per device per host thread/stream; a context is not re-entrant.
+ *   - One context per device per host thread/stream; a context is not re-entrant.  Its work is
+ *     ordered across streams by the library: an entry point that uses the context's scratch, called
+ *     on a stream other than the previous such call's, waits (device side) for that call's work, so
+ *     two streams sharing one context serialise; independent streams want one context each.
  */
 #ifndef FT8HIP_H
 #define FT8HIP_H

@@ -64,3 +64,40 @@ def test_counters_survive_reallocation(gpu, oracle):
     got = [r.tobytes() for r in dec.records(x)]   # one chain again, on the grown buffer
     assert got == want_recs
     check_bp(ctx)
+
+
+def test_one_context_on_alternating_streams(gpu):
+    """One context driven from two torch streams in turn with no host synchronisation: every call
+    waits (device side) for the previous call's work when the stream changes (capi.hip
+    StreamOrder), so each step's records equal a synchronous decode's.  Without that order two
+    steps' kernels would share the scratch and the k_bp claim counter concurrently."""
+    import torch
+    from ft8_demodulator_amd import _lib, synth
+    from ft8_demodulator_amd._pipeline import SlotDecoder
+    x, _ = synth.make_slots(16, 50, seed=6262, device="cuda")
+    ref = SlotDecoder(12000, 2, 2, **KW)
+    ref.ctx = _lib.Context(0)
+    out, counts = ref.run(x)
+    want, want_counts = out.clone(), counts.clone()
+    torch.cuda.synchronize()
+    assert int(want_counts.sum()) > 0
+    # two decoders (own output buffers, one per stream) on ONE context
+    ctx = _lib.Context(0)
+    decs = [SlotDecoder(12000, 2, 2, **KW), SlotDecoder(12000, 2, 2, **KW)]
+    for d in decs:
+        d.ctx = ctx
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    outs = []
+    for k in range(12):
+        with torch.cuda.stream(streams[k % 2]):
+            out, counts = decs[k % 2].run(x)
+            outs.append((out.clone(), counts.clone()))  # before this stream's next step reuses them
+    torch.cuda.synchronize()
+
+    def valid(out, counts):  # each slot's written records (the rest of the buffer is never written)
+        rec = out.cpu().numpy().view(_lib.RESULT_DTYPE).reshape(16, -1)
+        return [rec[i, : int(c)].tobytes() for i, c in enumerate(counts.cpu().numpy())]
+    want_recs = valid(want, want_counts)
+    for k, (out, counts) in enumerate(outs):
+        assert torch.equal(counts, want_counts), k
+        assert valid(out, counts) == want_recs, k
