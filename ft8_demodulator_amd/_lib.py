@@ -251,8 +251,9 @@ class Context:
         self.check(lib().ft8_get_timing(self.handle, ms, cnt, int(reset)), "ft8_get_timing")
         return {STAGE_NAMES[i]: (ms[i], cnt[i]) for i in range(N_STAGES)}
 
-    def set_pipeline(self, chunk_slots: int = 0, n_streams: int = 0, bp_waves_per_simd: int = 2):
-        """ft8_decode_batch chunking over internal streams (n_streams = 0: one chain)."""
+    def set_pipeline(self, chunk_slots: int = 0, n_streams: int = 0, bp_waves_per_simd: int = 4):
+        """ft8_decode_batch chunking over internal streams (n_streams = 0: one chain) and the BP
+        grid's resident waves per SIMD (1..4)."""
         self.check(lib().ft8_set_pipeline(self.handle, int(chunk_slots), int(n_streams), int(bp_waves_per_simd)),
                    "ft8_set_pipeline")
 

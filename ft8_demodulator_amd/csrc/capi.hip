@@ -82,7 +82,7 @@ struct ft8_ctx {
   int64_t launches[FT8_N_STAGES] = {0};
   // decode_batch pipeline: slot chunks spread over internal streams (0 = one chain on the caller's
   // stream); BP grid residency in waves per SIMD
-  int chunk_slots = 0, n_streams = 0, bp_waves = 2;
+  int chunk_slots = 0, n_streams = 0, bp_waves = 4;
   std::vector<hipStream_t> streams;
   hipEvent_t fork = nullptr;
   std::vector<hipEvent_t> joins;
@@ -740,7 +740,7 @@ int decode_pass(ft8_ctx* c, const void* d_samples, int dtype, int64_t n_samples,
     B.work_base = &c->work_base[1 + k];
     B.stats = (unsigned long long*)c->stats.p;
     B.clock = c->timing && c->stats.p ? (unsigned long long*)c->stats.p + 4 : nullptr;
-    B.grid_waves = n_str > 0 ? c->bp_waves : 8;  // clamped to the kernel's 4 resident waves per SIMD
+    B.grid_waves = c->bp_waves;  // resident waves per SIMD of the persistent grid (kernel maximum 4)
     B.tie = tie;
     B.warn = warn;
     StageTimer t6(c, 6, cs);

@@ -203,10 +203,11 @@ int ft8_decode_batch(ft8_ctx* ctx, const void* d_samples, int dtype, int64_t n_s
  * chunk_slots slots, each an independent STFT -> sync/select -> LLR -> BP -> compact chain, and
  * the chunks alternate over n_streams internal streams (forked from and joined back into the
  * caller's stream), so one chunk's BP overlaps the next chunk's STFT/score.  bp_waves_per_simd
- * (1..4) bounds the BP kernel's resident waves when pipelining, leaving room for the other
- * stream.  n_streams = 0 runs the whole batch as one chain on the caller's stream.  Default
- * (0, 0, 2): one chain -- on MI355X the BP kernel is FP64-VALU bound and overlapping it with the
- * next chunk's STFT/score measured no gain.  Results do not depend on the setting. */
+ * (1..4) bounds the BP kernel's resident waves per SIMD (chunked or not), leaving room for work on
+ * other streams.  n_streams = 0 runs the whole batch as one chain on the caller's stream.  Default
+ * (0, 0, 4): one chain, the full BP grid -- on MI355X the BP kernel is FP64-VALU bound and
+ * overlapping it with the next chunk's STFT/score measured no gain.  Results do not depend on the
+ * setting. */
 int ft8_set_pipeline(ft8_ctx* ctx, int32_t chunk_slots, int32_t n_streams, int32_t bp_waves_per_simd);
 
 /* ---- multi-GPU exchange (slot shards, one all-gather of the decodes per batch) --

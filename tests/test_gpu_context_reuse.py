@@ -60,7 +60,7 @@ def test_counters_survive_reallocation(gpu, oracle):
         got = [r.tobytes() for r in dec.records(x)]
         assert got == want_recs
     finally:
-        ctx.set_pipeline(0, 0, 2)
+        ctx.set_pipeline()
     got = [r.tobytes() for r in dec.records(x)]   # one chain again, on the grown buffer
     assert got == want_recs
     check_bp(ctx)

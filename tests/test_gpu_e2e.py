@@ -162,7 +162,7 @@ def test_pipeline_settings_do_not_change_results(gpu):
     x, _ = synth.make_slots(40, 30, seed=4242, device="cuda")
     dec = SlotDecoder(12000, 2, 2, 100, 3, 20)
     got = {}
-    for cfg in [(0, 0, 4), (8, 2, 2), (16, 3, 1), (7, 2, 4)]:
+    for cfg in [(0, 0, 4), (0, 0, 2), (8, 2, 2), (16, 3, 1), (7, 2, 4)]:
         dec.ctx.set_pipeline(*cfg)
         out, cnt = dec.run(x)
         got[cfg] = (out.cpu().numpy().tobytes(), cnt.cpu().numpy().tobytes())
