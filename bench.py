@@ -1253,7 +1253,9 @@ def main():
             per_rank = [None] * world
             dist.all_gather_object(per_rank, mine)
         gather["shard_parity"] = per_rank
-        gather["shard_parity_ok"] = all(p_ is not None and p_["payload_crc_multiset_equal"] for p_ in per_rank)
+        # None when no rank had an oracle sample (e.g. --no-cpu at N = 1): nothing was compared
+        gather["shard_parity_ok"] = (None if all(p_ is None for p_ in per_rank) else
+                                     all(p_ is not None and p_["payload_crc_multiset_equal"] for p_ in per_rank))
 
     total_slots = S * world * args.steps
     value = total_slots / elapsed
