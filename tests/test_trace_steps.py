@@ -1,0 +1,63 @@
+"""tools/trace_steps.py on synthetic kernel traces: one chain, and two streams whose steps overlap
+(bench --depth 2) followed by the one-chain loop -- the tool must find every step on its own
+stream, take the timed ones after max(warmup, depth), and report the loop period."""
+import csv
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KERNELS = ("ft8::k_stft3840p<float, true>", "ft8::k_score2<2, 2, true>", "ft8::k_select<float>",
+           "ft8::k_llr<float>", "ft8::k_bp<false>", "ft8::k_compact")
+DUR = (150, 220, 30, 80, 1500, 5)  # us
+
+
+def _write(tmp, steps, depth, warmup, K):
+    """steps: list of (stream, t0_us) -> trace csv + bench line."""
+    rows, did = [], 0
+    for sid, t0 in steps:
+        t = t0
+        for name, d in zip(KERNELS, DUR):
+            did += 1
+            rows.append({"Kind": "KERNEL_DISPATCH", "Stream_Id": sid, "Dispatch_Id": did, "Kernel_Name": name,
+                         "Start_Timestamp": int(t * 1000), "End_Timestamp": int((t + d) * 1000)})
+            t += d
+    trace = os.path.join(tmp, "trace.csv")
+    with open(trace, "w", newline="") as f:
+        w = csv.DictWriter(f, fieldnames=list(rows[0]))
+        w.writeheader()
+        w.writerows(rows)
+    line = {"warmup": warmup, "steps": K, "ms_per_step": 1.9, "depth": {"contexts": depth},
+            "roofline": {"launch_ms": 1.5, "flops_per_launch": 2.3e10, "peak": 78.6},
+            "stages_ms": {"stft": 0.15, "score": 0.22, "select": 0.03, "llr": 0.08, "bp": 1.5, "compact": 0.005}}
+    lf = os.path.join(tmp, "line.log")
+    with open(lf, "w") as f:
+        f.write(json.dumps(line) + "\n")
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "trace_steps.py"), trace, lf],
+                         capture_output=True, text=True, check=True)
+    return json.loads(out.stdout)
+
+
+def test_one_chain(tmp_path):
+    step = sum(DUR)
+    steps = [(0, i * step) for i in range(3 + 4)]
+    d = _write(str(tmp_path), steps, depth=1, warmup=3, K=4)
+    assert d["timed_steps"] == 4 and d["decode_steps_found"] == 7
+    assert abs(d["timed_period_ms_mean"] - step / 1000) < 1e-9
+    assert d["kernels_compared"] == "timed steps"
+    assert abs(d["timed_kernels_ms_mean"]["k_bp"] - 1.5) < 1e-9
+
+
+def test_two_streams_then_one_chain(tmp_path):
+    step = sum(DUR)
+    period = 1800  # overlapped steps: a new one every 1.8 ms on alternating streams
+    W, K = 5, 6
+    steps = [(1 + (i % 2), i * period) for i in range(W + K)]
+    t = (W + K) * period + step
+    steps += [(0, t + i * step) for i in range(K)]          # the one-chain loop after it
+    d = _write(str(tmp_path), steps, depth=2, warmup=W, K=K)
+    assert d["depth"] == 2 and d["timed_steps"] == K and d["decode_steps_found"] == W + 2 * K
+    assert abs(d["timed_period_ms_mean"] - ((K - 1) * period + step) / K / 1000) < 1e-9
+    assert abs(d["one_chain_period_ms_mean"] - step / 1000) < 1e-9
+    assert d["kernels_compared"] == "one-chain steps after the loop" and d["one_chain_steps_after_loop"] == K
