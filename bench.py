@@ -1118,9 +1118,7 @@ def main():
     # own stream -- so consecutive steps overlap only where the hardware lets them (the next step's
     # front end filling the CUs k_bp's last waves leave); every step still decodes the whole batch
     D = max(1, args.depth)
-    decs = [dec] + [SlotDecoder(12000, 2, 2, device=dev, **kw) for _ in range(D - 1)]
-    for d_ in decs[1:]:
-        d_.ctx = _lib.Context(local)
+    decs = [dec] + [SlotDecoder(12000, 2, 2, device=dev, context=_lib.Context(local), **kw) for _ in range(D - 1)]
     streams = [torch.cuda.current_stream(dev)] if D == 1 else [torch.cuda.Stream(dev) for _ in range(D)]
     for d_ in decs:
         d_.ctx.set_timing(True)   # allocates the device BP work counters; no events in the timed loop

@@ -199,7 +199,7 @@ class SlotDecoder:
 
     def __init__(self, sample_rate=12000, bins_per_tone=2, steps_per_symbol=2, max_candidates=20,
                  min_score=10, max_iterations=20, freq_min=None, freq_max=None, time_min=None,
-                 time_max=None, device=None, flags=0, max_results_per_slot=None):
+                 time_max=None, device=None, flags=0, max_results_per_slot=None, context=None):
         self.kw = dict(sample_rate=sample_rate, bins_per_tone=bins_per_tone, steps_per_symbol=steps_per_symbol,
                        freq_min=freq_min, freq_max=freq_max, time_min=time_min, time_max=time_max)
         self.max_candidates = int(max_candidates)
@@ -207,7 +207,10 @@ class SlotDecoder:
         self.max_iterations = int(max_iterations)
         self.flags = flags
         self.device = _lib.device_index(device)
-        self.ctx = _lib.context(self.device)
+        # the thread's context for the device, or a dedicated one (_lib.Context(device)): decoders
+        # that run concurrently on different streams want one context each (the library orders a
+        # shared context's work across streams, which serialises them)
+        self.ctx = context if context is not None else _lib.context(self.device)
         # a subtract-and-redecode batch appends up to max_candidates pass-2 records after up to
         # max_candidates pass-1 records, so its default capacity holds both passes
         default_cap = max(self.max_candidates, 1) * (2 if flags & _lib.FT8_FLAG_SUBTRACT else 1)
