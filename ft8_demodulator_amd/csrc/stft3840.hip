@@ -185,6 +185,32 @@ __device__ __forceinline__ void dft16_half(const f2* x, f2* y) {
   }
 }
 
+// 16-point DFT of x[0], x[1] with x[2..15] = 0: y[k] = x0 + W_16^k x1, y[k + 8] = x0 - W_16^k x1
+// (k < 8), y in natural order -- the first stage of a frame whose window covers at most 2 of the 16
+// inputs per butterfly (k_stft_pk's 9 600-point plan at 12 kHz: 1 920 samples of the 9 600-pair
+// half)
+__device__ __forceinline__ void dft16_two(f2 x0, f2 x1, f2* y) {
+  const f2 r = splat(0.70710678118654752440f);
+  const f2 t1 = cmul(x1, w16(1)), t3 = cmul(x1, w16(3)), t5 = cmul(x1, w16(5)), t7 = cmul(x1, w16(7));
+  const f2 t2 = add_mi(x1, x1) * r;  // x1 W_8 = r (x1.x + x1.y, x1.y - x1.x)
+  y[0] = x0 + x1;
+  y[8] = x0 - x1;
+  y[4] = add_mi(x0, x1);             // W_16^4 = -i
+  y[12] = sub_mi(x0, x1);
+  y[2] = x0 + t2;
+  y[10] = x0 - t2;
+  y[6] = add_mi(x0, t2);             // W_16^6 = -i W_16^2
+  y[14] = sub_mi(x0, t2);
+  y[1] = x0 + t1;
+  y[9] = x0 - t1;
+  y[3] = x0 + t3;
+  y[11] = x0 - t3;
+  y[5] = x0 + t5;
+  y[13] = x0 - t5;
+  y[7] = x0 + t7;
+  y[15] = x0 - t7;
+}
+
 template <typename InT>
 __device__ __forceinline__ f2 load_pair(const InT* x, int64_t n0) {
   if constexpr (sizeof(InT) == 4) {
@@ -563,6 +589,9 @@ __global__ __launch_bounds__(TH) void k_stft_pk(PkArgs a) {
   const InT* xslot = reinterpret_cast<const InT*>(a.samples) + (int64_t)slot * a.slot_stride;
   constexpr float kDb = 3.0102999566398119521f;  // 10 log10(v) = (10 log10 2) log2(v), v >= 1e-12
   const float qscale = 0.25f * a.scale;          // |2 X|^2 / 4 / (sum w)^2
+  // at most two nonzero inputs per stage-1 butterfly (n0 = 2 (j + r P / 16) >= nperseg for r >= 2):
+  // the pruned 16-point DFT (workgroup-uniform)
+  const bool two = a.nperseg <= 4 * NBF;
 #pragma unroll 1
   for (int fi = f_begin; fi < f_end; ++fi) {
     if (fi > f_begin) __syncthreads();  // the previous frame's epilogue has read the image
@@ -582,19 +611,22 @@ __global__ __launch_bounds__(TH) void k_stft_pk(PkArgs a) {
           }
         } else {
           // one frame per workgroup (the 9 600-point plan: its 1 920-sample window covers a fifth of
-          // the transformed half):
-          // per-lane branches, so the zero part's loads are skipped
+          // the transformed half): per-lane branches, so the zero part's loads are skipped
+          const int rn = two ? 2 : 8;
 #pragma unroll
           for (int r = 0; r < 8; ++r) {
             const int n0 = 2 * (j + r * NBF);
-            if (n0 + 1 < a.nperseg) {
+            if (r >= rn) {
+              z[r] = f2{0.0f, 0.0f};
+            } else if (n0 + 1 < a.nperseg) {
               z[r] = *reinterpret_cast<const f2*>(a.window + n0) * load_pair<InT>(xs, n0);
             } else {
               z[r] = f2{n0 < a.nperseg ? a.window[n0] * load_pair<InT>(xs, n0).x : 0.0f, 0.0f};
             }
           }
         }
-        dft16_half(z, y);
+        if (FR == 1 && two) dft16_two(z[0], z[1], y);
+        else dft16_half(z, y);
 #pragma unroll
         for (int k = 0; k < 16; ++k) lds_st(&buf[17 * j + k], y[k]);  // pidx(16 j + k)
       }
