@@ -2,7 +2,7 @@
 # profiles/ so the bench line reads this build's counters), the bench line.
 #   usage: bash tools/gpu_r5final_a.sh TAG   (TAG r<round>_v<k>; copy gpurun_out/TAG_pmc*.json into profiles/ here)
 set -o pipefail
-T=${1:-r5_v2}
+T=${1:-r5_v3}
 R=$GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest tests -x -v -rP --timeout 300 --timeout-method thread -m gpu > gpurun_out/${T}_tests.log 2>&1 &&

@@ -1,7 +1,7 @@
 # Round-5 final pass, part B: the headline kernel trace, the subtract-leg profile, the GPU suite on
 # the barrier-race check build (variants/RACE.so, tools/build_race.sh), the 2-rank rehearsal.
 set -o pipefail
-T=${1:-r5_v2}
+T=${1:-r5_v3}
 R=$GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 bash tools/gpu_prof.sh ${T} &&
