@@ -101,3 +101,29 @@ def test_one_context_on_alternating_streams(gpu):
     for k, (out, counts) in enumerate(outs):
         assert torch.equal(counts, want_counts), k
         assert valid(out, counts) == want_recs, k
+
+
+def test_two_contexts_on_two_streams(gpu):
+    """The bench's --depth 2 configuration: consecutive steps alternate over two decoders with their
+    own contexts and streams, so steps overlap on the device; every step's records equal a
+    synchronous decode's."""
+    import torch
+    from ft8_demodulator_amd import _lib, synth
+    from ft8_demodulator_amd._pipeline import SlotDecoder
+    x, _ = synth.make_slots(16, 50, seed=7373, device="cuda")
+    ref = SlotDecoder(12000, 2, 2, **KW)
+    want = ref.records(x)
+    assert sum(len(r) for r in want) > 0
+    want = [r.tobytes() for r in want]
+    decs = [SlotDecoder(12000, 2, 2, context=_lib.Context(0), **KW) for _ in range(2)]
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    outs = []
+    for k in range(10):
+        with torch.cuda.stream(streams[k % 2]):
+            out, counts = decs[k % 2].run(x)
+            outs.append((out.clone(), counts.clone()))
+    torch.cuda.synchronize()
+    for k, (out, counts) in enumerate(outs):
+        rec = out.cpu().numpy().view(_lib.RESULT_DTYPE).reshape(16, -1)
+        got = [rec[i, : int(c)].tobytes() for i, c in enumerate(counts.cpu().numpy())]
+        assert got == want, k
