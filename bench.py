@@ -21,6 +21,8 @@ is the first shard of every larger run.
 Prints ONE JSON line on rank 0.  Besides the contract fields it carries:
   depth         contexts / streams the timed steps alternate over; one_chain: the same K steps on one
                 context and one stream, timed after the loop (N=1)
+  settle        untimed steps run before the W warmup steps until consecutive blocks' GPU times agree
+                within 1.5 % (k_bp's clock ramp), their block times; --settle_max 0 turns it off
   roofline      the dominant kernel (k_bp: LLR + float64 BP + CRC), FLOP-rate vs the FP64 vector peak
   roofline_hbm  the HBM-bound STFT kernel, GB/s vs the 8 TB/s HBM peak
   stages_ms     per-kernel device time per step (HIP events on the decode stream)
@@ -834,29 +836,62 @@ def drift_correct(dev, n_sig=256, reps=5):
             "data": "synthetic (HIP transmit chain, reference GFSK timing; seeded drift and noise)"}
 
 
-def h2d_stream(x, steps, kw):
+def h2d_stream(x, steps, kw, depth=2):
     """Slots handed over as 16-bit PCM in pinned host memory (the WAV ingestion path): the upload of
-    batch k+1 on a copy stream overlaps the decode of batch k.  PCIe-inclusive slots/s -- reported
-    beside `value`, never as it."""
+    batch k+depth on a copy stream overlaps the decodes of the batches before it, which alternate
+    over `depth` decoders/streams as the headline's steps do.  PCIe-inclusive slots/s -- reported
+    beside `value`, never as it -- with the leg's two bounds: the upload alone (PCIe) and the same
+    pipeline at depth 1."""
     import torch
     from ft8_demodulator_amd.stream import StreamDecoder
     pcm = torch.clamp(torch.round(x / x.abs().amax() * 30000.0), -32767, 32767).to(torch.int16).cpu().pin_memory()
     S = pcm.shape[0]
-    sd = StreamDecoder(pcm.shape[1], max_batch=S, **kw)
-    for _ in sd.decode_batches([pcm] * steps):  # warm-up: the first stream of a process pays one-time costs
-        pass
+
+    def run(sd):
+        for _ in sd.decode_batches([pcm] * 6):  # warm-up: the first stream of a process pays one-time costs
+            pass
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ts = []
+        for _ in sd.decode_batches([pcm] * steps):
+            ts.append(time.perf_counter())
+        torch.cuda.synchronize()
+        # steady state: the spacing of batches' results once the pipeline is full (after the first
+        # NBUF yields, before the drain's last ones, which come back to back)
+        lo, hi = sd.NBUF, steps - sd.NBUF
+        steady = (ts[hi] - ts[lo]) / (hi - lo) if hi > lo else None
+        return (time.perf_counter() - t0) / steps, steady
+
+    dt, steady = run(StreamDecoder(pcm.shape[1], max_batch=S, depth=depth, **kw))
+    dt1, steady1 = run(StreamDecoder(pcm.shape[1], max_batch=S, depth=1, **kw)) if depth > 1 else (dt, steady)
+    # the PCIe bound: the same pinned batch uploaded back to back on its own
+    dbuf = torch.empty(pcm.shape, dtype=pcm.dtype, device=x.device)
+    for _ in range(3):
+        dbuf.copy_(pcm, non_blocking=True)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in sd.decode_batches([pcm] * steps):
-        pass
+    for _ in range(steps):
+        dbuf.copy_(pcm, non_blocking=True)
     torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
+    up = (time.perf_counter() - t0) / steps
+    del dbuf
+    nbytes = int(pcm.numel() * 2)
     return {"workload": f"{steps} batches of {S} int16 PCM slots handed over in pinned host memory "
-                        "(ft8_demodulator_amd.stream.StreamDecoder): batch k+2 uploads on a copy stream "
-                        "while batch k+1 decodes and batch k's results are copied back to pinned host "
-                        "memory and converted to the reference's result tuples",
-            "slots_per_s": S * steps / dt, "ms_per_batch": dt / steps * 1e3,
-            "h2d_bytes_per_batch": int(pcm.numel() * 2)}
+                        f"(ft8_demodulator_amd.stream.StreamDecoder, depth {depth}): batch k+{depth + 1} uploads on "
+                        f"a copy stream while batches k+1..k+{depth} decode on {depth} contexts/streams "
+                        "and batch k's results are copied back to pinned host memory and converted to the "
+                        "reference's result tuples",
+            "slots_per_s": S / dt, "ms_per_batch": dt * 1e3, "depth": depth,
+            "timing": f"wall clock over the {steps} batches (pipeline fill and drain included)",
+            "steady": None if steady is None else {
+                "slots_per_s": S / steady, "ms_per_batch": steady * 1e3,
+                "what": "spacing of consecutive batches' results with the pipeline full"},
+            "depth1": {"slots_per_s": S / dt1, "ms_per_batch": dt1 * 1e3,
+                       "steady_ms_per_batch": None if steady1 is None else steady1 * 1e3},
+            "h2d_bytes_per_batch": nbytes,
+            "upload_alone": {"ms_per_batch": up * 1e3, "gb_per_s": nbytes / up / 1e9,
+                             "slots_per_s": S / up,
+                             "what": "the pinned batch copied to the device back to back, nothing else running"}}
 
 
 def single_call(x, calls=50):
@@ -1013,6 +1048,9 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--slots", type=int, default=256, help="slots per GPU per step")
+    ap.add_argument("--settle_max", type=int, default=96,
+                    help="untimed steps at most before the warmup, until the GPU time of consecutive "
+                         "blocks of 4*depth steps agrees within 1.5%% (k_bp's clock ramp); 0 = off")
     ap.add_argument("--depth", type=int, default=2,
                     help="consecutive steps alternate over this many contexts, each on its own stream, so one "
                          "step's STFT / sync can start while the previous step's k_bp retires its last waves "
@@ -1142,6 +1180,35 @@ def main():
                 ev.record()             # on this step's stream, after its work
         return counts
 
+    # clock settling before the W warmup steps: k_bp's shader clock ramps over its first launches
+    # (step_times of the driver's --warmup 5 lines: the first timed pairs 10 % slower than the last),
+    # so untimed blocks of 4 D steps run until a block's GPU time is within 1.5 % of the one before
+    # (at most --settle_max steps; 0 = off).  Reported in the line as `settle`.
+    settle = {"steps": 0, "block_ms": [], "max_steps": args.settle_max}
+    if args.settle_max > 0:
+        blk = 4 * D
+        ev_a, ev_b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        prev = None
+        while settle["steps"] + blk <= args.settle_max:
+            torch.cuda.synchronize()
+            ev_a.record()
+            for k_ in range(blk):
+                step(k_)
+            for st_ in streams:
+                torch.cuda.current_stream(dev).wait_stream(st_)
+            ev_b.record()
+            torch.cuda.synchronize()
+            t_ = ev_a.elapsed_time(ev_b)
+            settle["steps"] += blk
+            settle["block_ms"].append(round(t_, 4))
+            done_ = prev is not None and abs(t_ - prev) <= 0.015 * prev
+            if world > 1:   # every rank runs the same settle steps (each step's exchange is a collective)
+                flag_ = torch.tensor([0.0 if done_ else 1.0], device=dev)
+                dist.all_reduce(flag_, op=dist.ReduceOp.MAX)
+                done_ = flag_.item() == 0.0
+            if done_:
+                break
+            prev = t_
     for k_ in range(max(args.warmup, D)):
         step(k_)
     torch.cuda.synchronize()
@@ -1304,7 +1371,7 @@ def main():
         stress = bp_stress(ctx, dev, procs=host_cores()[0])
     stream = None
     if world == 1 and not args.no_h2d:
-        stream = h2d_stream(x, max(3, min(args.steps, 10)), kw)
+        stream = h2d_stream(x, 40, kw, depth=D)
     call = single_call(x) if world == 1 else None
     drift = None
     if world == 1 and not args.no_drift:
@@ -1385,6 +1452,7 @@ def main():
                      "clock": bp_clock, "issue": issue},
         "step_times": step_times,
         "depth": {"contexts": D, "streams": D if D > 1 else 1, "one_chain": depth1},
+        "settle": settle,
         "step_hbm": {"what": "BASELINE.md whole-step accounting: slots/s per GPU x B_slot algorithmic bytes "
                              "(the step is FP64-VALU bound in k_bp, so this fraction is low by construction)",
                      "bytes_per_slot": b_slot, "achieved": step_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",

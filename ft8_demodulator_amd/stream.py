@@ -2,9 +2,12 @@
 pipelining").
 
 Batches of 15-s slots -- typically 16-bit PCM straight from WAV files -- are staged in pinned host
-memory and uploaded on a dedicated copy stream into one of three device buffers: batch k + 2 uploads
-while batch k + 1 decodes on the compute stream and batch k's results are converted on the host;
-results come back through pinned host buffers.  int16 PCM
+memory and uploaded on a dedicated copy stream into one of depth + 2 device buffers: the copy stream
+uploads batch k + depth + 1 while batches k + 1 .. k + depth decode and batch k's results are
+converted on the host; results come back through pinned host buffers.  Consecutive batches decode on
+`depth` decoders (default 2), each with its own library context and compute stream, so the next
+batch's front end (STFT, sync, selection) runs in the CUs the previous batch's k_bp tail leaves --
+the bench's `--depth` pattern (bench.py).  int16 PCM
 is uploaded as-is (half the PCIe bytes of float32) and scaled by the STFT kernel exactly as
 read_wave_file does (from_wave.py:59-67).
 
@@ -25,12 +28,11 @@ from ._pipeline import SlotDecoder, records_to_results, warn_truncated
 
 
 class StreamDecoder:
-    """Triple-buffered host -> device upload overlapped with ft8_decode_batch."""
-
-    NBUF = 3
+    """Host -> device upload on a copy stream overlapped with ft8_decode_batch on `depth` decoders
+    (own context and compute stream each; depth 1 = one decoder on the current stream)."""
 
     def __init__(self, n_samples: int, sample_rate: int = 12000, max_batch: int = 256, pcm16: bool = True,
-                 device=None, **decoder_kw):
+                 device=None, depth: int = 2, **decoder_kw):
         torch = _lib.require_gpu()
         self.torch = torch
         self.dev = torch.device("cuda", _lib.device_index(device))
@@ -39,11 +41,23 @@ class StreamDecoder:
         self.max_batch = int(max_batch)
         self.pcm16 = bool(pcm16)
         self.dtype = torch.int16 if pcm16 else torch.float32
+        self.depth = int(depth)
+        if self.depth < 1:
+            raise ValueError("depth must be >= 1")
+        self.NBUF = self.depth + 2   # depth decoding + one uploading + the one being collected
         self.dec = SlotDecoder(sample_rate=sample_rate, device=self.dev, **decoder_kw)
+        # decoders 1 .. depth-1 own a context each: decoders sharing one would be ordered across
+        # their streams by the library (one chain again)
+        self.decs = [self.dec] + [SlotDecoder(sample_rate=sample_rate, device=self.dev,
+                                              context=_lib.Context(self.dev.index), **decoder_kw)
+                                  for _ in range(self.depth - 1)]
         self.bpt = self.dec.kw["bins_per_tone"]
         self.code = _lib.FT8_I16 if pcm16 else _lib.FT8_F32
         self.copy_stream = torch.cuda.Stream(self.dev)
-        self.compute = torch.cuda.current_stream(self.dev)
+        self.computes = ([torch.cuda.current_stream(self.dev)] if self.depth == 1 else
+                         [torch.cuda.Stream(self.dev) for _ in range(self.depth)])
+        self.compute = self.computes[0]
+        self.uploaded = [None] * self.NBUF   # copy-stream event: dbuf[i] holds its batch
         self.dbuf = [torch.empty((self.max_batch, self.n), dtype=self.dtype, device=self.dev) for _ in range(self.NBUF)]
         self.hbuf = [torch.empty((self.max_batch, self.n), dtype=self.dtype, pin_memory=True) for _ in range(self.NBUF)]
         self.freed = [None] * self.NBUF   # compute-stream event: decode done with dbuf[i]
@@ -68,7 +82,7 @@ class StreamDecoder:
                 self.dbuf[i][:nb].copy_(src, non_blocking=True)
                 up = torch.cuda.Event()
                 up.record(self.copy_stream)
-            self.compute.wait_event(up)
+            self.uploaded[i] = up
             self.caller_upload = up  # the caller's buffer is read until this completes
             return nb
         b = np.asarray(batch)
@@ -87,21 +101,25 @@ class StreamDecoder:
             self.dbuf[i][:nb].copy_(self.hbuf[i][:nb], non_blocking=True)
             up = torch.cuda.Event()
             up.record(self.copy_stream)
-        self.compute.wait_event(up)
+        self.uploaded[i] = up
         return nb
 
-    def _launch(self, i: int, nb: int):
+    def _launch(self, i: int, nb: int, k: int):
+        """Decode buffer i (batch k) on decoder / stream k % depth, after its upload."""
         torch = self.torch
-        with torch.cuda.stream(self.compute):
-            out, cnt = self.dec.run(self.dbuf[i][:nb], code=self.code)
+        st = self.computes[k % self.depth]
+        dec = self.decs[k % self.depth]
+        st.wait_event(self.uploaded[i])
+        with torch.cuda.stream(st):
+            out, cnt = dec.run(self.dbuf[i][:nb], code=self.code)
             ev = torch.cuda.Event()
-            ev.record(self.compute)
+            ev.record(st)
             self.freed[i] = ev
-            cap = self.dec.cap * _lib.RESULT_DTYPE.itemsize
+            cap = dec.cap * _lib.RESULT_DTYPE.itemsize
             self.hout[i][: nb * cap].copy_(out[: nb * cap], non_blocking=True)
             self.hcnt[i][:nb].copy_(cnt[:nb], non_blocking=True)
             r = torch.cuda.Event()
-            r.record(self.compute)
+            r.record(st)
             self.ready[i] = r
 
     def _collect(self, i: int, nb: int) -> List[list]:
@@ -123,10 +141,11 @@ class StreamDecoder:
         return out
 
     def decode_batches(self, batches: Iterable) -> Iterator[List[list]]:
-        """Yield per-slot results of each batch, in order.  Two batches are in flight on the device:
-        when batch k's decode ends, batch k + 1 (already uploaded) decodes while batch k + 2 uploads
-        and batch k's results are converted.  A pinned caller tensor is uploaded in place, and its
-        upload has completed before control returns to the caller (who may refill it)."""
+        """Yield per-slot results of each batch, in order.  depth + 2 batches are in flight on the
+        device: when batch k's decode ends, batches k + 1 .. k + depth decode (on their own
+        streams, overlapping) while batch k + depth + 1 uploads and batch k's results are converted.  A
+        pinned caller tensor is uploaded in place, and its upload has completed before control
+        returns to the caller (who may refill it)."""
         it = iter(batches)
         end = object()
         launched = []   # (buffer, n_slots), oldest first
@@ -138,7 +157,7 @@ class StreamDecoder:
             count += 1
             self.caller_upload = None
             nb = self._stage(i, batch)
-            self._launch(i, nb)
+            self._launch(i, nb, count - 1)
             launched.append((i, nb))
             return self.caller_upload
 
@@ -151,9 +170,11 @@ class StreamDecoder:
                 up.synchronize()
         while launched:
             i, nb = launched[0]
-            self.ready[i].synchronize()     # the oldest batch's decode and result copy are done
+            # the next upload goes out before the oldest batch is waited for: its buffer's previous
+            # batch was collected last iteration, so the copy stream never idles behind a decode
             batch = next(it, end)
             up = start(batch) if batch is not end else None
+            self.ready[i].synchronize()     # the oldest batch's decode and result copy are done
             done = self._collect(i, nb)     # conversion overlaps the new upload
             launched.pop(0)
             if up is not None:

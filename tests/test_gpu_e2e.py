@@ -183,12 +183,20 @@ def test_stream_decoder_matches_resident_decode(gpu):
     pcm = torch.clamp(torch.round(x / x.abs().amax() * 30000.0), -32767, 32767).to(torch.int16).cpu().numpy()
     kw = dict(max_candidates=100, min_score=3, max_iterations=20)
     ref = SlotDecoder(12000, **kw).decode(torch.from_numpy(pcm).cuda())
-    sd = StreamDecoder(pcm.shape[1], max_batch=8, **kw)
-    got = []
-    for res in sd.decode_batches([pcm[0:8], pcm[8:16], pcm[16:24]]):
-        got.extend(res)
     key = lambda rs: [[(m.payload.hex(), s.crc_calculated, t, f, float(sc)) for (m, s, t, f, sc) in r] for r in rs]
-    assert key(got) == key(ref)
+    # depth 1 (one decoder), 2 (the default: two contexts/streams) and 3; ragged last batches
+    for depth in (1, 2, 3):
+        sd = StreamDecoder(pcm.shape[1], max_batch=8, depth=depth, **kw)
+        got = []
+        for res in sd.decode_batches([pcm[0:8], pcm[8:16], pcm[16:21], pcm[21:24]]):
+            got.extend(res)
+        assert key(got) == key(ref), depth
+        # a second pass over the same decoder (buffers and events reused), as pinned tensors
+        got = []
+        pinned = torch.from_numpy(pcm).pin_memory()
+        for res in sd.decode_batches([pinned[0:8], pinned[8:16], pinned[16:24]]):
+            got.extend(res)
+        assert key(got) == key(ref), depth
     assert sum(len(r) for r in got) > 0
     from ft8_demodulator_amd import decode_ft8_from_wave
     wavs = [os.path.join(DATA, n) for n in ("synth_cfg1.wav", "synth_cfg2.wav")]
