@@ -140,12 +140,15 @@ class StreamDecoder:
             pos += c
         return out
 
-    def decode_batches(self, batches: Iterable) -> Iterator[List[list]]:
+    def decode_batches(self, batches: Iterable, borrow: bool = False) -> Iterator[List[list]]:
         """Yield per-slot results of each batch, in order.  depth + 2 batches are in flight on the
         device: when batch k's decode ends, batches k + 1 .. k + depth decode (on their own
         streams, overlapping) while batch k + depth + 1 uploads and batch k's results are converted.  A
         pinned caller tensor is uploaded in place, and its upload has completed before control
-        returns to the caller (who may refill it)."""
+        returns to the caller (who may refill it).  borrow=True: a pinned caller tensor is instead
+        lent to the decoder until its own batch's results are yielded (a caller cycling through at
+        least depth + 3 pinned buffers, or never rewriting them, may pass it), so no upload is
+        waited for on the host and the copy stream runs uploads back to back."""
         it = iter(batches)
         end = object()
         launched = []   # (buffer, n_slots), oldest first
@@ -166,7 +169,7 @@ class StreamDecoder:
             if batch is end:
                 break
             up = start(batch)
-            if up is not None:
+            if up is not None and not borrow:
                 up.synchronize()
         while launched:
             i, nb = launched[0]
@@ -177,7 +180,7 @@ class StreamDecoder:
             self.ready[i].synchronize()     # the oldest batch's decode and result copy are done
             done = self._collect(i, nb)     # conversion overlaps the new upload
             launched.pop(0)
-            if up is not None:
+            if up is not None and not borrow:
                 up.synchronize()
             yield done
 

@@ -197,6 +197,11 @@ def test_stream_decoder_matches_resident_decode(gpu):
         for res in sd.decode_batches([pinned[0:8], pinned[8:16], pinned[16:24]]):
             got.extend(res)
         assert key(got) == key(ref), depth
+        # lent pinned batches (no host wait on uploads)
+        got = []
+        for res in sd.decode_batches([pinned[0:8], pinned[8:16], pinned[16:21], pinned[21:24]], borrow=True):
+            got.extend(res)
+        assert key(got) == key(ref), depth
     assert sum(len(r) for r in got) > 0
     from ft8_demodulator_amd import decode_ft8_from_wave
     wavs = [os.path.join(DATA, n) for n in ("synth_cfg1.wav", "synth_cfg2.wav")]

@@ -21,4 +21,6 @@ if __name__ == "__main__":
             print(json.dumps({"round": rnd, "depth": depth, "ms_per_batch": round(r["ms_per_batch"], 4),
                               "slots_per_s": round(r["slots_per_s"]),
                               "steady_ms": round(r["steady"]["ms_per_batch"], 4),
+                              "borrow_ms": round(r["borrow"]["ms_per_batch"], 4),
+                              "borrow_steady_ms": round(r["borrow"]["steady_ms_per_batch"], 4),
                               "upload_alone_ms": round(r["upload_alone"]["ms_per_batch"], 4)}), flush=True)
