@@ -836,6 +836,11 @@ def drift_correct(dev, n_sig=256, reps=5):
             "data": "synthetic (HIP transmit chain, reference GFSK timing; seeded drift and noise)"}
 
 
+def settled(prev_ms, cur_ms, tol=0.015):
+    """The settle phase's stop rule: a block's GPU time within `tol` of the previous block's."""
+    return prev_ms is not None and abs(cur_ms - prev_ms) <= tol * prev_ms
+
+
 def h2d_stream(x, steps, kw, depth=2):
     """Slots handed over as 16-bit PCM in pinned host memory (the WAV ingestion path): the upload of
     batch k+depth on a copy stream overlaps the decodes of the batches before it, which alternate
@@ -1210,7 +1215,7 @@ def main():
             t_ = ev_a.elapsed_time(ev_b)
             settle["steps"] += blk
             settle["block_ms"].append(round(t_, 4))
-            done_ = prev is not None and abs(t_ - prev) <= 0.015 * prev
+            done_ = settled(prev, t_)
             if world > 1:   # every rank runs the same settle steps (each step's exchange is a collective)
                 flag_ = torch.tensor([0.0 if done_ else 1.0],
                                      device="cpu" if dist.get_backend() == "gloo" else dev)

@@ -111,3 +111,13 @@ def test_bp_cpu_baseline_threads(bench):
     assert out["cores"] == 3 and out["kind"] == "port" and out["value"] > 0
     assert out["extrapolated_s_per_launch"] == 100000 / out["value"]
     assert out["sample"].startswith("24 of")
+
+
+def test_settle_stop_rule(bench):
+    """The clock-settle phase stops on the first block within 1.5 % of the one before (the driver's
+    --warmup 5 lines showed the first timed pairs ~10 % slower than the last)."""
+    blocks = [33.0, 15.9, 15.0, 14.95]
+    stops = [i for i in range(1, len(blocks)) if bench.settled(blocks[i - 1], blocks[i])]
+    assert stops == [3]
+    assert not bench.settled(None, 15.0)
+    assert bench.settled(15.0, 15.2) and not bench.settled(15.0, 15.3)
