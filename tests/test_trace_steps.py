@@ -13,7 +13,7 @@ KERNELS = ("ft8::k_stft3840p<float, true>", "ft8::k_score2<2, 2, true>", "ft8::k
 DUR = (150, 220, 30, 80, 1500, 5)  # us
 
 
-def _write(tmp, steps, depth, warmup, K):
+def _write(tmp, steps, depth, warmup, K, settle=None):
     """steps: list of (stream, t0_us) -> trace csv + bench line."""
     rows, did = [], 0
     for sid, t0 in steps:
@@ -31,6 +31,8 @@ def _write(tmp, steps, depth, warmup, K):
     line = {"warmup": warmup, "steps": K, "ms_per_step": 1.9, "depth": {"contexts": depth},
             "roofline": {"launch_ms": 1.5, "flops_per_launch": 2.3e10, "peak": 78.6},
             "stages_ms": {"stft": 0.15, "score": 0.22, "select": 0.03, "llr": 0.08, "bp": 1.5, "compact": 0.005}}
+    if settle is not None:
+        line["settle"] = {"steps": settle, "block_ms": [], "max_steps": 96}
     lf = os.path.join(tmp, "line.log")
     with open(lf, "w") as f:
         f.write(json.dumps(line) + "\n")
@@ -61,3 +63,17 @@ def test_two_streams_then_one_chain(tmp_path):
     assert abs(d["timed_period_ms_mean"] - ((K - 1) * period + step) / K / 1000) < 1e-9
     assert abs(d["one_chain_period_ms_mean"] - step / 1000) < 1e-9
     assert d["kernels_compared"] == "one-chain steps after the loop" and d["one_chain_steps_after_loop"] == K
+
+
+def test_settle_steps_precede_the_warmup(tmp_path):
+    """The bench's clock-settle steps (line `settle.steps`) run before the warmup: the timed loop
+    starts after settle + max(warmup, depth) steps.  Settle steps here are spaced 3 ms apart, the
+    rest one step apart, so a wrong offset shows in the period."""
+    step = sum(DUR)
+    S, W, K = 8, 3, 4
+    steps = [(0, i * 3000) for i in range(S)]
+    t0 = S * 3000
+    steps += [(0, t0 + i * step) for i in range(W + K)]
+    d = _write(str(tmp_path), steps, depth=1, warmup=W, K=K, settle=S)
+    assert d["warmup"] == S + W and d["timed_steps"] == K and d["decode_steps_found"] == S + W + K
+    assert abs(d["timed_period_ms_mean"] - step / 1000) < 1e-9

@@ -4,7 +4,7 @@
 
 Finds the decode steps in dispatch order on each stream (k_stft* -> k_score* -> k_select -> k_llr ->
 k_bp -> k_compact; with `--depth D` consecutive steps run on D streams), orders them by their first
-dispatch, takes steps W .. W+K-1 as the timed loop (W = max(the line's warmup, depth), K = its
+dispatch, takes steps W .. W+K-1 as the timed loop (W = the line's settle steps + max(its warmup, depth), K = its
 `steps`), and reports per timed step the sum of kernel durations and the device span (first kernel
 start -> last kernel end), and for the loop its device period (first timed kernel start -> last
 timed kernel end, / K), against the line's ms_per_step; then every k_bp dispatch in order (decode
@@ -36,7 +36,9 @@ def main():
     with open(a.line) as f:
         line = next(json.loads(l) for l in f if l.startswith("{"))
     depth = int(line.get("depth", {}).get("contexts", 1) or 1)
-    W = max(line["warmup"], depth) if a.warmup is None else a.warmup
+    # steps before the timed loop: the clock-settle phase's (bench `settle`, round 5), then the warmup
+    settle = int((line.get("settle") or {}).get("steps", 0) or 0)
+    W = settle + max(line["warmup"], depth) if a.warmup is None else a.warmup
     K = line["steps"]
     rows = []
     with open(a.trace) as f:
