@@ -710,7 +710,13 @@ def sensitivity(dev, rates=None, snr_lo=-24.0, snr_hi=-5.0, step=0.2, rounds=20,
             j = hit[0]
             r0, r1 = ratio[j - 1], ratio[j]
             cross = float(snrs[j - 1] + (0.5 - r0) / (r1 - r0) * (snrs[j] - snrs[j - 1])) if r1 > r0 else float(snrs[j])
-        row = {"fs": fs, "bandwidth_hz": fs / 2, "min_snr_db": thr, "crossing_50pct_db": cross,
+        # the reference harness's own rule on its own grid (test_ft8_standard.py:74-76, 81-82:
+        # np.arange(-21, -10, 0.2); 3 when no point reaches 50 %) -- the wider grid is an extension
+        on_ref = (snrs >= -21.0 - 1e-9) & (snrs < -10.0 - 1e-9)
+        hit_ref = np.nonzero(on_ref & (ok >= rounds * 0.5))[0]
+        ref_rule = float(snrs[hit_ref[0]]) if hit_ref.size else 3.0
+        row = {"fs": fs, "bandwidth_hz": fs / 2, "min_snr_db": thr, "ref_rule_min_snr_db": ref_rule,
+               "crossing_50pct_db": cross,
                "xlsx_min_snr_db": XLSX_MIN_SNR_DB.get(fs),
                "success_per_point": {f"{s_:.1f}": int(k_) for s_, k_ in zip(snrs, ok) if 0 < k_ < rounds}}
         table.append(row)
@@ -731,9 +737,11 @@ def sensitivity(dev, rates=None, snr_lo=-24.0, snr_hi=-5.0, step=0.2, rounds=20,
     mism = [{"fs": fs_, "snr_db": s_, "gpu": g_, "oracle": c_} for (fs_, s_, _x, g_), c_ in zip(samples, cpu) if g_ != c_]
     return {"method": "test_ft8_standard.py:43-123 on the GPU: f0 = fc = 0, bins_per_tone = steps_per_symbol = 2, "
                       "K = 20, min_score 1, 20 iterations, float64 input; SNR over the full band (B = fs / 2); "
-                      f"{snr_lo} .. {snr_hi} dB in {step} dB steps, {rounds} rounds per point; min_snr_db = the "
-                      "first point with >= 50 % decodes (the reference's rule), crossing_50pct_db = the linear "
-                      "interpolation of the success ratio at 0.5",
+                      f"{snr_lo} .. {snr_hi} dB in {step} dB steps (an extension of the reference's "
+                      "np.arange(-21, -10, 0.2) grid), {rounds} rounds per point; min_snr_db = the first point with "
+                      ">= 50 % decodes on the wide grid; ref_rule_min_snr_db = the reference's rule on its own grid "
+                      "(3 when no point of it reaches 50 %); crossing_50pct_db = the linear interpolation of the "
+                      "success ratio at 0.5",
             "rounds": rounds, "slots": n_dec_slots, "decode_slots_per_s": n_dec_slots / t_dec if t_dec else None,
             "table": table,
             "parity": {"slots": len(samples), "equal": len(samples) - len(mism), "mismatches": mism[:8],
@@ -1054,6 +1062,122 @@ def launch_ranks(args):
     return subprocess.call(cmd, env=env)
 
 
+LINE_MAX = 4096   # bytes of the stdout line; the driver's parser gave up on the 23.8 KB r05 line
+
+
+def _strict(o, nd=None):
+    """JSON-safe copy: NaN / +-inf -> None (strict JSON), numpy scalars -> Python, floats rounded to
+    `nd` significant digits when given (the compact line)."""
+    import math
+    if isinstance(o, dict):
+        return {str(k): _strict(v, nd) for k, v in o.items()}
+    if isinstance(o, (list, tuple)):
+        return [_strict(v, nd) for v in o]
+    if hasattr(o, "item") and not isinstance(o, (str, bytes)):
+        try:
+            o = o.item()
+        except (TypeError, ValueError):
+            return str(o)
+    if isinstance(o, bool) or o is None or isinstance(o, (int, str)):
+        return o
+    if isinstance(o, float):
+        if not math.isfinite(o):
+            return None
+        return float(f"{o:.{nd}g}") if nd else o
+    return str(o)
+
+
+def write_legs(full, path):
+    """The full record (every leg, step times, per-rank shard parity) -> `path` (relative to the repo
+    root unless absolute), strict JSON.  -> the path as the line names it (None if unwritable)."""
+    p = path if os.path.isabs(path) else os.path.join(ROOT, path)
+    try:
+        os.makedirs(os.path.dirname(p) or ".", exist_ok=True)
+        with open(p, "w") as f:
+            json.dump(_strict(full), f, allow_nan=False, indent=1)
+    except OSError as e:
+        print(f"bench.py: could not write {p}: {e}", file=sys.stderr)
+        return None
+    return path
+
+
+def _pick(d, keys):
+    return None if d is None else {k: d.get(k) for k in keys if k in d}
+
+
+def compact_line(full, legs_path):
+    """The one stdout line: the contract fields, roofline, cpu_baseline, a parity summary, settle steps,
+    the one-chain rate, build id and (N > 1) the exchange's two verdicts; per-leg headline numbers
+    only, every leg's full record in the side file `legs`.  Strict JSON, <= LINE_MAX bytes."""
+    rf = full.get("roofline") or {}
+    clk = rf.get("clock") or {}
+    rh = full.get("roofline_hbm") or {}
+    par = full.get("parity")
+    one = (full.get("depth") or {}).get("one_chain")
+    line = {k: full.get(k) for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup")}
+    line["settle_steps"] = full.get("settle_steps", (full.get("settle") or {}).get("steps", 0))
+    for k in ("ms_per_step", "higher_is_better", "scaling", "vs_baseline", "dtype", "data"):
+        line[k] = full.get(k)
+    if "rehearsal" in full:
+        line["rehearsal"] = full["rehearsal"]
+    cfg = full.get("config") or {}
+    line["config"] = {k: cfg.get(k) for k in ("workload", "slots_per_gpu", "sample_rate", "max_candidates",
+                                              "min_score", "max_iterations", "pipeline_depth", "parallelism")
+                      if k in cfg}
+    line["ldpc_candidates_per_s"] = full.get("ldpc_candidates_per_s")
+    line["decodes_per_step"] = full.get("decodes_per_step")
+    line["roofline"] = {**_pick(rf, ("kernel", "bound", "achieved", "peak", "unit", "frac", "traffic",
+                                     "traffic_source", "launch_ms", "flops_per_launch")),
+                        "clock_effective_ghz": clk.get("effective_ghz")}
+    line["roofline_hbm"] = _pick(rh, ("kernel", "bound", "achieved", "peak", "unit", "frac", "traffic",
+                                      "launch_ms", "bytes_per_launch"))
+    line["cpu_baseline"] = _pick(full.get("cpu_baseline"), ("value", "unit", "cores", "kind", "sample"))
+    line["parity"] = None if par is None else {
+        "slots": par.get("slots"), "equal": par.get("payload_crc_multiset_equal"),
+        "decodes_gpu": par.get("decodes_gpu"), "decodes_cpu": par.get("decodes_cpu"),
+        "ordered_equal_slots": par.get("ordered_lists_equal_slots")}
+    line["depth"] = {"contexts": (full.get("depth") or {}).get("contexts"),
+                     "one_chain_value": None if one is None else one.get("value")}
+    g = full.get("gather")
+    if g is not None:
+        line["gather"] = {"backend": g.get("backend"), "world": g.get("world"), "gather_ok": g.get("gather_ok"),
+                          "shard_parity_ok": g.get("shard_parity_ok")}
+    gn = full.get("gather_n1")
+    if gn:
+        line["gather_n1_ms_per_step"] = {k: gn.get(k) for k in ("ms_per_step_plain", "ms_per_step_with_gather")
+                                         if k in gn}
+    legs = {}
+    bs = full.get("bp_stress")
+    if bs:
+        legs["bp_stress_candidates_per_s"] = bs.get("candidates_per_s")
+    sr = full.get("subtract_redecode")
+    if sr:
+        legs["subtract_redecode_candidates_per_s"] = sr.get("candidates_per_s")
+    hs = full.get("h2d_stream")
+    if hs:
+        legs["h2d_stream_slots_per_s"] = hs.get("slots_per_s")
+    dc = full.get("drift_correct")
+    if dc:
+        legs["drift_signals_per_s"] = dc.get("signals_per_s")
+    if legs:
+        line["legs_summary"] = legs
+    line["build_id"] = full.get("build_id")
+    line["gpu_clock_ghz"] = full.get("gpu_clock_ghz")
+    line["legs"] = legs_path
+    out = _strict(line, nd=6)
+    s = json.dumps(out, allow_nan=False, separators=(",", ":"))
+    # over budget (long free-text fields): shed the descriptive strings first, never the numbers
+    for k in ("data", "legs_summary", "roofline_hbm"):
+        if len(s.encode()) <= LINE_MAX:
+            break
+        out.pop(k, None)
+        s = json.dumps(out, allow_nan=False, separators=(",", ":"))
+    if len(s.encode()) > LINE_MAX and out.get("cpu_baseline"):
+        out["cpu_baseline"].pop("sample", None)
+        s = json.dumps(out, allow_nan=False, separators=(",", ":"))
+    return s
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -1083,13 +1207,18 @@ def main():
                     help="slots of the subtract leg checked against oracle/subtract.py (0: none)")
     ap.add_argument("--no-drift", action="store_true", help="skip the frequency-drift correction leg")
     ap.add_argument("--no-geometries", action="store_true", help="skip the 20 kHz / bpt=10 geometry legs")
-    ap.add_argument("--no-sensitivity", action="store_true",
-                    help="skip the reference's sensitivity harness (test_ft8_standard.py) on the GPU")
+    ap.add_argument("--no-sensitivity", action="store_true", help=argparse.SUPPRESS)  # the leg is opt-in now
+    ap.add_argument("--sensitivity", action="store_true",
+                    help="also run the reference's sensitivity harness (test_ft8_standard.py) on the GPU "
+                         "(~36k float64 slot decodes + an oracle sample; opt-in, into the legs file)")
     ap.add_argument("--gather", action="store_true",
                     help="N = 1: every timed step also packs its decodes and all-gathers them over a world-size-1 "
                          "RCCL group (the per-step exchange of the N > 1 path)")
     ap.add_argument("--no-gather-leg", action="store_true",
                     help="skip the N = 1 leg that times steps with and without the RCCL exchange")
+    ap.add_argument("--legs-out", default=os.path.join("gpurun_out", "bench_legs.json"),
+                    help="side file (relative to the repo root unless absolute) that receives the full record: "
+                         "every leg, step times, per-rank shard parity; the stdout line names it")
     ap.add_argument("--share-gpu", action="store_true",
                     help="rehearsal of the N > 1 path on a one-GPU box: every rank on cuda:0, gloo instead of "
                          "RCCL (exercises the launch, sharding and decode gather; not a measurement)")
@@ -1397,7 +1526,7 @@ def main():
     if world == 1 and not args.no_geometries:
         geoms = geometry_legs(dev)
     sens = None
-    if world == 1 and not args.no_sensitivity:
+    if world == 1 and args.sensitivity:
         sens = sensitivity(dev, procs=host_cores()[0])
     sub = None
     if world == 1 and not args.no_subtract:
@@ -1498,8 +1627,11 @@ def main():
         line["gather"] = gather
     if gather_n1 is not None:
         line["gather_n1"] = gather_n1
+    line["settle_steps"] = settle["steps"]
     if rank == 0:
-        print(json.dumps(line), flush=True)
+        # every leg goes to the side file; stdout gets ONE compact line (<= LINE_MAX bytes, strict JSON)
+        legs_path = write_legs(line, args.legs_out)
+        print(compact_line(line, legs_path), flush=True)
     if dist.is_initialized():
         dist.destroy_process_group()
 

@@ -180,7 +180,8 @@ def stft(wave_data, sample_rate, bins_per_tone, steps_per_symbol, f_lo=None, f_h
         return None, plan, f64
     ctx = _lib.context(x.device)
     p = _lib.Ft8Params()
-    p.sample_rate, p.bins_per_tone, p.steps_per_symbol = int(sample_rate), int(bins_per_tone), int(steps_per_symbol)
+    p.sample_rate_hz = _lib.sample_rate_hz(sample_rate)
+    p.sample_rate, p.bins_per_tone, p.steps_per_symbol = int(p.sample_rate_hz), int(bins_per_tone), int(steps_per_symbol)
     p.f_lo = 0 if f_lo is None else int(f_lo)
     p.f_hi = plan.nfft if f_hi is None else int(f_hi)
     p.t_lo = 0 if t_lo is None else int(t_lo)

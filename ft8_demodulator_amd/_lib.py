@@ -34,7 +34,7 @@ class Ft8Params(ctypes.Structure):
                 ("max_iterations", ctypes.c_int32), ("min_score_f64", ctypes.c_int32),
                 ("min_score", ctypes.c_double), ("f_lo", ctypes.c_int32), ("f_hi", ctypes.c_int32),
                 ("t_lo", ctypes.c_int32), ("t_hi", ctypes.c_int32), ("flags", ctypes.c_int32),
-                ("reserved", ctypes.c_int32)]
+                ("reserved", ctypes.c_int32), ("sample_rate_hz", ctypes.c_double)]
 
 
 class Ft8DriftParams(ctypes.Structure):
@@ -111,6 +111,7 @@ def lib():
             "ft8_abi_version": ([], ctypes.c_int),
             "ft8_limits": ([vp, vp, vp], ctypes.c_int),
             "ft8_geometry": ([i32, i32, i32, i64, vp, vp, vp, vp], ctypes.c_int),
+            "ft8_geometry_hz": ([dbl, i32, i32, i64, vp, vp, vp, vp], ctypes.c_int),
             "ft8_stft": ([vp, vp, ctypes.c_int, i64, i32, i64, P, vp, vp], ctypes.c_int),
             "ft8_sync_select": ([vp, vp, ctypes.c_int, i32, i32, i32, P, vp, vp, vp, vp, vp], ctypes.c_int),
             "ft8_llr": ([vp, vp, ctypes.c_int, i32, i32, i32, i32, vp, i32, ctypes.c_int, vp, vp], ctypes.c_int),
@@ -183,6 +184,7 @@ def source_hash():
 
 EXPORTED_SYMBOLS = (
     "ft8_create", "ft8_destroy", "ft8_last_error", "ft8_abi_version", "ft8_limits", "ft8_geometry",
+    "ft8_geometry_hz",
     "ft8_stft", "ft8_sync_select", "ft8_llr", "ft8_normalize", "ft8_bp", "ft8_decode_batch", "ft8_select_warnings",
     "ft8_crc14", "ft8_ldpc_check", "ft8_set_timing", "ft8_get_timing", "ft8_get_counters", "ft8_get_bp_clock", "ft8_set_pipeline",
     "ft8_encode", "ft8_synthesize", "ft8_subtract", "ft8_stft_argmax", "ft8_drift_fit", "ft8_drift_correct",
@@ -196,11 +198,21 @@ def limits():
     return {"max_candidates": a.value, "max_fft_real": b.value, "max_fft_complex": c.value}
 
 
-def geometry(sample_rate: int, bins_per_tone: int, steps_per_symbol: int, n_samples: int):
-    """(nperseg, hop, nfft, frames) of calculate_spectrogram (spectrogram_analyse.py:31-43)."""
+def sample_rate_hz(sample_rate) -> float:
+    """The sample rate as the reference uses it: any positive finite number of Hz, integral or not
+    (spectrogram_analyse.py:32-34 computes int(0.16 fs) and int(fs / 6.25 bpt) on the value given)."""
+    fs = float(sample_rate)
+    if not (0.0 < fs < 2e9):
+        raise ValueError(f"sample_rate must be a positive finite number of Hz, got {sample_rate!r}")
+    return fs
+
+
+def geometry(sample_rate, bins_per_tone: int, steps_per_symbol: int, n_samples: int):
+    """(nperseg, hop, nfft, frames) of calculate_spectrogram (spectrogram_analyse.py:31-43), computed
+    by the library from the float sample rate."""
     v = [ctypes.c_int32() for _ in range(4)]
-    rc = lib().ft8_geometry(int(sample_rate), int(bins_per_tone), int(steps_per_symbol), int(n_samples),
-                            *[ctypes.byref(x) for x in v])
+    rc = lib().ft8_geometry_hz(sample_rate_hz(sample_rate), int(bins_per_tone), int(steps_per_symbol),
+                               int(n_samples), *[ctypes.byref(x) for x in v])
     if rc != FT8_OK:
         raise ValueError("invalid spectrogram geometry (nfft must be greater than or equal to nperseg, "
                          "positive sample rate and oversampling factors)")

@@ -23,7 +23,7 @@ FT8_SYMBOL_FREQ_INTERVAL_HZ = 6.25  # spectrogram_analyse.py:7
 
 @dataclass
 class Plan:
-    sample_rate: int
+    sample_rate: float  # as the caller gave it (int or float Hz)
     bins_per_tone: int
     steps_per_symbol: int
     n_samples: int
@@ -94,7 +94,9 @@ def min_score_is_f64(min_score) -> bool:
 
 def make_params(plan: Plan, max_candidates, min_score, max_iterations, flags=0) -> _lib.Ft8Params:
     p = _lib.Ft8Params()
-    p.sample_rate = int(plan.sample_rate)
+    fs = _lib.sample_rate_hz(plan.sample_rate)
+    p.sample_rate = int(fs)
+    p.sample_rate_hz = fs   # the geometry follows the float rate (spectrogram_analyse.py:32-34)
     p.bins_per_tone = int(plan.bins_per_tone)
     p.steps_per_symbol = int(plan.steps_per_symbol)
     p.max_candidates = int(max_candidates)

@@ -488,11 +488,16 @@ struct Geo {
   int nperseg, hop, noverlap, nfft, frames;
 };
 
-int geometry(int fs, int bpt, int sps, int64_t n, Geo* g, std::string* why) {
-  if (fs <= 0 || bpt <= 0 || sps <= 0) { *why = "sample_rate, bins_per_tone and steps_per_symbol must be positive"; return FT8_E_ARG; }
-  g->nperseg = (int)(0.16 * (double)fs);                 // spectrogram_analyse.py:32
+// the sample rate a parameter block names: the exact Hz when given (ABI 2), else the integral field
+double rate_of(const ft8_params* p) { return p->sample_rate_hz > 0.0 ? p->sample_rate_hz : (double)p->sample_rate; }
+
+// fs in double: the reference computes both lengths on the float it was given (a float fs such as
+// 10e3 or 12006.3 is legal there), so int(0.16 * 12006.3) = 1921, not int(0.16 * 12006) = 1920
+int geometry(double fs, int bpt, int sps, int64_t n, Geo* g, std::string* why) {
+  if (!(fs > 0.0) || !(fs < 2e9) || bpt <= 0 || sps <= 0) { *why = "sample_rate, bins_per_tone and steps_per_symbol must be positive"; return FT8_E_ARG; }
+  g->nperseg = (int)(0.16 * fs);                         // spectrogram_analyse.py:32
   g->noverlap = g->nperseg - g->nperseg / sps;           // :33
-  g->nfft = (int)((double)fs / 6.25 * (double)bpt);      // :34
+  g->nfft = (int)(fs / 6.25 * (double)bpt);              // :34
   if (g->noverlap >= g->nperseg) g->noverlap = g->nperseg - 1;  // :42-43
   g->hop = g->nperseg - g->noverlap;
   if (g->nperseg < 1) { *why = "nperseg must be a positive integer"; return FT8_E_ARG; }
@@ -508,7 +513,7 @@ int do_stft(ft8_ctx* c, const void* samples, int dtype, int64_t n_samples, int n
             const ft8_params* p, void* d_wf, hipStream_t s) {
   Geo g;
   std::string why;
-  int rc = geometry(p->sample_rate, p->bins_per_tone, p->steps_per_symbol, n_samples, &g, &why);
+  int rc = geometry(rate_of(p), p->bins_per_tone, p->steps_per_symbol, n_samples, &g, &why);
   if (rc) return fail(c, rc, why);
   if (dtype < FT8_F32 || dtype > FT8_I16) return fail(c, FT8_E_ARG, "unknown sample dtype");
   if (p->t_lo < 0 || p->t_hi > g.frames || p->t_lo > p->t_hi)
@@ -815,7 +820,7 @@ int subtract_core(ft8_ctx* c, const void* x, int dtype, float* resid, int64_t n_
                   const int32_t* counts, int cap, hipStream_t s) {
   Geo g;
   std::string why;
-  int rc = geometry(p->sample_rate, p->bins_per_tone, p->steps_per_symbol, n_samples, &g, &why);
+  int rc = geometry(rate_of(p), p->bins_per_tone, p->steps_per_symbol, n_samples, &g, &why);
   if (rc) return fail(c, rc, why);
   if (dtype != FT8_F32 && dtype != FT8_I16) return fail(c, FT8_E_UNSUPPORTED, "subtraction needs float32 or int16 samples");
   if (x_stride != r_stride) return fail(c, FT8_E_ARG, "residual and sample strides differ");
@@ -833,7 +838,7 @@ int subtract_core(ft8_ctx* c, const void* x, int dtype, float* resid, int64_t n_
   L.n_samples = n_samples;
   L.slot_stride = x_stride;
   L.n_slots = n_slots;
-  L.fs = p->sample_rate;
+  L.fs = rate_of(p);
   L.nsps = g.nperseg;
   L.hop = g.hop;
   L.nfft = g.nfft;
@@ -868,7 +873,7 @@ int stft_argmax_core(ft8_ctx* c, const void* x, int dtype, int64_t n_samples, in
                      const ft8_params* p, int32_t* idx, hipStream_t s) {
   Geo g;
   std::string why;
-  int rc = geometry(p->sample_rate, p->bins_per_tone, p->steps_per_symbol, n_samples, &g, &why);
+  int rc = geometry(rate_of(p), p->bins_per_tone, p->steps_per_symbol, n_samples, &g, &why);
   if (rc) return fail(c, rc, why);
   if (dtype < FT8_F32 || dtype > FT8_I16) return fail(c, FT8_E_ARG, "unknown sample dtype");
   if (p->t_lo < 0 || p->t_hi > g.frames || p->t_lo > p->t_hi)
@@ -1072,6 +1077,11 @@ const char* ft8_last_error(const ft8_ctx* c) { return c ? c->err.c_str() : "null
 
 int ft8_geometry(int32_t fs, int32_t bpt, int32_t sps, int64_t n, int32_t* nperseg, int32_t* hop, int32_t* nfft,
                  int32_t* frames) {
+  return ft8_geometry_hz((double)fs, bpt, sps, n, nperseg, hop, nfft, frames);
+}
+
+int ft8_geometry_hz(double fs, int32_t bpt, int32_t sps, int64_t n, int32_t* nperseg, int32_t* hop, int32_t* nfft,
+                    int32_t* frames) {
   Geo g;
   std::string why;
   int rc = geometry(fs, bpt, sps, n, &g, &why);
@@ -1230,7 +1240,7 @@ int ft8_decode_batch(ft8_ctx* c, const void* d_samples, int dtype, int64_t n_sam
   StageTimer whole(c, 5, s);
   Geo g;
   std::string why;
-  int rc = geometry(p->sample_rate, p->bins_per_tone, p->steps_per_symbol, n_samples, &g, &why);
+  int rc = geometry(rate_of(p), p->bins_per_tone, p->steps_per_symbol, n_samples, &g, &why);
   if (rc) return fail(c, rc, why);
   const int T = p->t_hi - p->t_lo, F = p->f_hi - p->f_lo;
   const bool f64 = is_f64_dtype(dtype);

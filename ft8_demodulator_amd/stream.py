@@ -37,7 +37,7 @@ class StreamDecoder:
         self.torch = torch
         self.dev = torch.device("cuda", _lib.device_index(device))
         self.n = int(n_samples)
-        self.fs = int(sample_rate)
+        self.fs = sample_rate   # as given (int or float Hz): result times are abs_time / fs
         self.max_batch = int(max_batch)
         self.pcm16 = bool(pcm16)
         self.dtype = torch.int16 if pcm16 else torch.float32

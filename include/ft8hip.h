@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define FT8HIP_ABI_VERSION 1
+#define FT8HIP_ABI_VERSION 2
 
 /* sample dtypes.  The waterfall dtype follows NumPy promotion against complex64 exactly as
  * scipy.signal.spectrogram does (spectrogram_analyse.py:46-56): F32/C64/I16 -> float32 waterfall,
@@ -61,6 +61,10 @@ typedef struct ft8_params {
   int32_t t_lo, t_hi;       /* kept frames [t_lo, t_hi) after the time mask */
   int32_t flags;            /* FT8_FLAG_* (0: the reference's behaviour exactly) */
   int32_t reserved;
+  double sample_rate_hz;    /* ABI 2: when > 0, the exact sample rate in Hz, integral or not (the
+                               reference takes a float fs: spectrogram_analyse.py:32-34 computes
+                               int(0.16 fs) and int(fs / 6.25 bpt) on it, so fs = 12006.3 gives
+                               nperseg 1921); sample_rate is then ignored.  0: use sample_rate. */
 } ft8_params;
 
 /* ft8_params.flags.  Both are build-defined extensions OUTSIDE reference parity (the reference
@@ -125,6 +129,10 @@ int ft8_limits(int32_t* max_candidates, int32_t* max_fft_real, int32_t* max_fft_
 int ft8_geometry(int32_t sample_rate, int32_t bins_per_tone, int32_t steps_per_symbol,
                  int64_t n_samples, int32_t* nperseg, int32_t* hop, int32_t* nfft,
                  int32_t* n_frames);
+/* The same for a sample rate given in (possibly non-integral) Hz, as ft8_params.sample_rate_hz. */
+int ft8_geometry_hz(double sample_rate_hz, int32_t bins_per_tone, int32_t steps_per_symbol,
+                    int64_t n_samples, int32_t* nperseg, int32_t* hop, int32_t* nfft,
+                    int32_t* n_frames);
 
 /* ---- stage 1: STFT -> dB waterfall ---------------------------------------------------------
  * Replaces calculate_spectrogram (spectrogram_analyse.py:19-66) + the f>=0 / band / time masks

@@ -121,3 +121,67 @@ def test_settle_stop_rule(bench):
     assert stops == [3]
     assert not bench.settled(None, 15.0)
     assert bench.settled(15.0, 15.2) and not bench.settled(15.0, 15.3)
+
+
+def _fixture(name):
+    root = os.path.dirname(os.path.abspath(__file__))
+    with open(os.path.join(root, "data", name)) as f:
+        return json.load(f)
+
+
+def _check_line(s, n_gpus):
+    assert len(s.encode()) <= 4096, len(s.encode())
+    assert "\n" not in s
+    d = json.loads(s, parse_constant=lambda c: (_ for _ in ()).throw(ValueError(c)))   # strict: no NaN/Infinity
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "settle_steps", "ms_per_step", "config",
+              "dtype", "roofline", "cpu_baseline", "parity", "depth", "build_id", "legs"):
+        assert k in d, k
+    assert d["n_gpus"] == n_gpus
+    for k in ("kernel", "achieved", "peak", "frac", "launch_ms", "traffic", "traffic_source", "clock_effective_ghz"):
+        assert k in d["roofline"], k
+    return d
+
+
+def test_compact_line_n1(bench):
+    """The r05 line (23.8 KB, which the driver could not parse) -> one strict-JSON line <= 4 KB with
+    the contract fields, roofline, cpu_baseline, a parity summary and the settle steps."""
+    full = _fixture("bench_full_n1_r5.json")
+    full["settle_steps"] = full["settle"]["steps"]
+    full["roofline"]["frac"] = float("nan")      # a non-finite number must not leak into the line
+    s = bench.compact_line(full, "gpurun_out/bench_legs.json")
+    d = _check_line(s, 1)
+    assert d["roofline"]["frac"] is None
+    assert d["value"] == pytest.approx(full["value"], rel=1e-5)
+    assert d["settle_steps"] == full["settle"]["steps"] and d["warmup"] == full["warmup"]
+    for k in ("value", "unit", "cores", "kind"):
+        assert d["cpu_baseline"][k] == pytest.approx(full["cpu_baseline"][k], rel=1e-5) \
+            if isinstance(full["cpu_baseline"][k], float) else d["cpu_baseline"][k] == full["cpu_baseline"][k]
+    assert d["parity"]["equal"] is True and d["parity"]["slots"] == full["parity"]["slots"]
+    assert d["depth"]["one_chain_value"] == pytest.approx(full["depth"]["one_chain"]["value"], rel=1e-5)
+    assert d["legs"] == "gpurun_out/bench_legs.json"
+
+
+def test_compact_line_n8(bench):
+    """A synthetic N = 8 record (the N = 4 rehearsal's, widened to 8 ranks with every per-rank array
+    and the legs at their largest) still gives a line <= 4 KB carrying only the exchange's verdicts."""
+    full = _fixture("bench_full_n4_r5.json")
+    g = full["gather"]
+    g["world"] = 8
+    g["shard_parity"] = [dict(g["shard_parity"][0], rank=r, mismatching_slots=list(range(32)))
+                         for r in range(8)]
+    g["decodes_per_rank_last_step"] = [12345] * 8
+    full["n_gpus"] = 8
+    full["settle_steps"] = 96
+    full["data"] = "x" * 3000                  # an over-long free-text field is shed, numbers stay
+    s = bench.compact_line(full, "/tmp/legs.json")
+    d = _check_line(s, 8)
+    assert set(d["gather"]) == {"backend", "world", "gather_ok", "shard_parity_ok"}
+    assert d["gather"]["world"] == 8 and d["settle_steps"] == 96
+
+
+def test_write_legs_strict(bench, tmp_path):
+    full = {"a": float("inf"), "b": [1.0, float("nan")], "c": np.float32(2.5), "d": np.int64(3)}
+    p = bench.write_legs(full, str(tmp_path / "legs" / "x.json"))
+    with open(p) as f:
+        txt = f.read()
+    assert json.loads(txt) == {"a": None, "b": [1.0, None], "c": 2.5, "d": 3}

@@ -23,7 +23,7 @@ def test_header_symbols_exported():
 
 def test_host_entry_points_without_gpu():
     from ft8_demodulator_amd import _lib
-    assert _lib.lib().ft8_abi_version() == 1
+    assert _lib.lib().ft8_abi_version() == 2
     assert _lib.geometry(12000, 2, 2, 180000) == (1920, 960, 3840, 186)
     assert _lib.geometry(20000, 2, 2, 252800) == (3200, 1600, 6400, 157)
     assert _lib.geometry(12000, 2, 2, 1000)[3] == 0

@@ -4,6 +4,10 @@
              (nfft 19 200: the direct-DFT STFT, the generic float64 score kernel), K = 20, min_score 5
   ref_6k     test_decode_ft8_message (:92-126): fs 6000, f0 = 0 (tones at DC), bpt = sps = 2,
              K = 20, min_score 1
+  nochan_*   test_ft8_without_channel.py:30-57: fs = 10e3 as a float, f0 = 550 Hz, -19..-15 dB,
+             bpt = sps = 4 (nfft 6400), K = 20, min_score 1
+  ref_fs_frac  a non-integral sample rate, fs = 12006.3: nperseg 1921, nfft 3842 (chirp-z), computed
+             on the float as spectrogram_analyse.py:32-34 does
 
 Goldens from the reference itself (tools/make_golden_reftests.py -> tests/golden/reftests.*), inputs
 stored as the reference's float64 samples.  CPU tests pin the oracle (waterfall SHA-256, score-grid
@@ -31,7 +35,8 @@ def _sha(a):
     return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
 
 
-CASES = ("ref_noise", "ref_6k")
+CASES = ("ref_noise", "ref_6k", "nochan_19db_s11", "nochan_17db_s12", "nochan_17db_s13", "nochan_15db_s14",
+         "ref_fs_frac")
 
 
 @pytest.mark.parametrize("name", CASES)
@@ -108,3 +113,18 @@ def test_gpu_decode_on_reference_test_geometry(reft, gpu, name):
         assert type(sc).__name__ == r["score_dtype"]
         # float64 input: a float64 FFT (1e-9); float32: a float32 FFT's rounding (1e-4)
         assert abs(float(sc) - r["score"]) <= (1e-9 if r["score_dtype"] == "float64" else 1e-4)
+
+
+def test_geometry_follows_the_float_sample_rate():
+    """spectrogram_analyse.py:32-34 on the float fs: int(0.16 * 12006.3) = 1921 (not 1920) and
+    int(12006.3 / 6.25 * 2) = 3842; fs = 10e3 as a float equals the integer rate."""
+    from ft8_demodulator_amd import _lib
+    from ft8_demodulator_amd._pipeline import make_plan
+    assert _lib.geometry(12006.3, 2, 2, 180000) == (1921, 960, 3842, (180000 - 961) // 960)
+    assert _lib.geometry(12006, 2, 2, 180000) == (1920, 960, 3841, (180000 - 960) // 960)
+    assert _lib.geometry(10e3, 4, 4, 126400) == _lib.geometry(10000, 4, 4, 126400) == (1600, 400, 6400, 313)
+    p = make_plan(180000, 12006.3)
+    assert (p.nperseg, p.nfft, p.F) == (1921, 3842, 1921)
+    for bad in (0, -1.0, float("nan"), float("inf")):
+        with pytest.raises(ValueError):
+            _lib.geometry(bad, 2, 2, 1000)

@@ -15,7 +15,16 @@ shape), its score grid's SHA-256 (ref_6k: full grid; ref_noise: the rows around 
 pinned by hash only), the candidate list with scores, normalised LLRs of the first candidates, and
 decode_ft8_message's results.
 
-Usage:  cd /tmp && python /root/repo/tools/make_golden_reftests.py
+  nochan_*   test_ft8_without_channel.py:30-57: fs = 10e3 (a FLOAT), f0 = 550 Hz, fc = 0, payload
+             np.random.randint(0, 255, 10) with [9] &= 0xF8, noise at the full-band SNR (-19 / -17 /
+             -15 dB), bins_per_tone = steps_per_symbol = 4 (nperseg 1600, hop 400, nfft 6400),
+             max_candidates 20, min_score 1, 20 iterations; several seeds
+  ref_fs_frac  the same decode call at a NON-INTEGRAL sample rate, fs = 12006.3 (f0 = 1000 Hz,
+             bpt = sps = 2, -15 dB): the reference computes int(0.16 fs) = 1921 and int(fs / 6.25 * 2)
+             = 3842 on the float (spectrogram_analyse.py:32-34)
+
+Usage:  cd /tmp && python /root/repo/tools/make_golden_reftests.py [nochannel]
+        (nochannel: add / replace only the nochan_* and ref_fs_frac cases in the existing files)
 """
 import contextlib
 import hashlib
@@ -100,9 +109,55 @@ def case(name, x, fs, kw, arrays, sub_rows=None):
     return c
 
 
+NOCHAN = [(-19, 11), (-17, 12), (-17, 13), (-15, 14)]   # (snr_db, np.random.seed)
+
+
+def nochannel_cases(arrays):
+    """test_ft8_without_channel.py:30-57 with np.random.seed(seed) before its draws, in its order:
+    payload (randint(0, 255, 10), [9] &= 0xF8), then the noise (randn)."""
+    out = []
+    for snr_db, seed in NOCHAN:
+        np.random.seed(seed)
+        p = np.random.randint(0, 255, size=10, dtype=np.uint8)
+        p[9] &= 0xF8
+        fs = 10e3
+        w = quiet(RG.ft8_generator, p, fs=fs, f0=550, fc=0)
+        noise = np.sqrt(np.mean(w ** 2) / (10 ** (snr_db / 10))) * np.random.randn(len(w))
+        x = w + noise
+        kw = dict(bins_per_tone=4, steps_per_symbol=4, max_candidates=20, min_score=1, max_iterations=20)
+        c = case(f"nochan_{-snr_db}db_s{seed}", x, fs, kw, arrays)
+        c["payload_sent"] = p.tobytes().hex()
+        out.append(c)
+    # a non-integral sample rate through the same call
+    np.random.seed(15)
+    p = np.random.randint(0, 255, size=10, dtype=np.uint8)
+    p[9] &= 0xF8
+    fs = 12006.3
+    w = quiet(RG.ft8_generator, p, fs=fs, f0=1000, fc=0)
+    x = w + np.sqrt(np.mean(w ** 2) / (10 ** (-15 / 10))) * np.random.randn(len(w))
+    kw = dict(bins_per_tone=2, steps_per_symbol=2, max_candidates=20, min_score=1, max_iterations=20)
+    c = case("ref_fs_frac", x, fs, kw, arrays, sub_rows=list(range(-20, 30)))
+    c["payload_sent"] = p.tobytes().hex()
+    out.append(c)
+    return out
+
+
 def main():
     scratch = tempfile.mkdtemp(prefix="ft8gold_")
     os.chdir(scratch)
+    if sys.argv[1:] == ["nochannel"]:
+        with open(os.path.join(GOLD, "reftests.json")) as f:
+            meta = json.load(f)
+        old = np.load(os.path.join(GOLD, "reftests.npz"), allow_pickle=False)
+        arrays = {k: old[k] for k in old.files}
+        new = nochannel_cases(arrays)
+        names = {c["name"] for c in new}
+        meta["cases"] = [c for c in meta["cases"] if c["name"] not in names] + new
+        np.savez_compressed(os.path.join(GOLD, "reftests.npz"), **arrays)
+        with open(os.path.join(GOLD, "reftests.json"), "w") as f:
+            json.dump(meta, f, indent=1, sort_keys=True)
+        print("updated", os.path.join(GOLD, "reftests.{json,npz}"))
+        return
     arrays, cases = {}, []
 
     # test_decode_with_noise (:128-163)
