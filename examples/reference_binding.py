@@ -34,7 +34,10 @@ class ft8_params(ctypes.Structure):
                 ("max_iterations", ctypes.c_int32), ("min_score_f64", ctypes.c_int32),
                 ("min_score", ctypes.c_double), ("f_lo", ctypes.c_int32), ("f_hi", ctypes.c_int32),
                 ("t_lo", ctypes.c_int32), ("t_hi", ctypes.c_int32), ("flags", ctypes.c_int32),
-                ("reserved", ctypes.c_int32)]
+                ("reserved", ctypes.c_int32), ("sample_rate_hz", ctypes.c_double)]
+
+
+FT8HIP_ABI_VERSION = 2   # include/ft8hip.h: ft8_params carries sample_rate_hz since ABI 2
 
 
 class ft8_result(ctypes.Structure):
@@ -45,7 +48,7 @@ class ft8_result(ctypes.Structure):
                 ("pad", ctypes.c_uint8)]
 
 
-assert ctypes.sizeof(ft8_result) == 40
+assert ctypes.sizeof(ft8_result) == 40 and ctypes.sizeof(ft8_params) == 64
 
 
 class _Backend:
@@ -62,9 +65,11 @@ class _Backend:
         self.ft8.ft8_create.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]
         self.ft8.ft8_last_error.argtypes = [vp]
         self.ft8.ft8_last_error.restype = ctypes.c_char_p
-        self.ft8.ft8_geometry.argtypes = [i32, i32, i32, i64, vp, vp, vp, vp]
+        self.ft8.ft8_geometry_hz.argtypes = [ctypes.c_double, i32, i32, i64, vp, vp, vp, vp]
         self.ft8.ft8_decode_batch.argtypes = [vp, vp, ctypes.c_int, i64, i32, i64, ctypes.POINTER(ft8_params),
                                               vp, vp, i32, vp]
+        if self.ft8.ft8_abi_version() != FT8HIP_ABI_VERSION:
+            raise RuntimeError(f"{lib_path}: ABI {self.ft8.ft8_abi_version()}, this binding speaks {FT8HIP_ABI_VERSION}")
         self._check_hip(self.hip.hipSetDevice(device), "hipSetDevice")
         self.ctx = vp()
         rc = self.ft8.ft8_create(device, ctypes.byref(self.ctx))
@@ -87,7 +92,8 @@ class _Backend:
 
     def geometry(self, fs, bpt, sps, n):
         v = [ctypes.c_int32() for _ in range(4)]
-        self._check(self.ft8.ft8_geometry(fs, bpt, sps, n, *[ctypes.byref(x) for x in v]), "ft8_geometry")
+        # the float rate, as spectrogram_analyse.py:32-34 uses it (fs = 10e3 or 12006.3 are legal there)
+        self._check(self.ft8.ft8_geometry_hz(float(fs), bpt, sps, n, *[ctypes.byref(x) for x in v]), "ft8_geometry_hz")
         return [x.value for x in v]
 
 
@@ -130,7 +136,8 @@ def decode_ft8_message(wave_data, sample_rate, bins_per_tone=2, steps_per_symbol
         return []
     f = np.fft.fftfreq(nfft, 1 / sample_rate)[: (nfft + 1) // 2]
     t = np.arange(nperseg / 2, n - nperseg / 2 + 1, hop) / float(sample_rate)
-    p = ft8_params(sample_rate=sample_rate, bins_per_tone=bins_per_tone, steps_per_symbol=steps_per_symbol,
+    p = ft8_params(sample_rate=int(sample_rate), sample_rate_hz=float(sample_rate),
+                   bins_per_tone=bins_per_tone, steps_per_symbol=steps_per_symbol,
                    max_candidates=max_candidates, max_iterations=max_iterations,
                    min_score_f64=int(isinstance(min_score, np.generic)
                                      and np.result_type(np.float32, min_score) == np.float64),

@@ -24,6 +24,14 @@ def test_header_symbols_exported():
 def test_host_entry_points_without_gpu():
     from ft8_demodulator_amd import _lib
     assert _lib.lib().ft8_abi_version() == 2
+    # ABI 2: ft8_params ends with the double sample_rate_hz (64 bytes); the example binding agrees
+    assert ctypes.sizeof(_lib.Ft8Params) == 64 and _lib.Ft8Params.sample_rate_hz.offset == 56
+    import importlib.util
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("rb", os.path.join(root, "examples", "reference_binding.py"))
+    rb = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(rb)
+    assert [f[0] for f in rb.ft8_params._fields_] == [f[0] for f in _lib.Ft8Params._fields_]
     assert _lib.geometry(12000, 2, 2, 180000) == (1920, 960, 3840, 186)
     assert _lib.geometry(20000, 2, 2, 252800) == (3200, 1600, 6400, 157)
     assert _lib.geometry(12000, 2, 2, 1000)[3] == 0
