@@ -1062,6 +1062,39 @@ def launch_ranks(args):
     return subprocess.call(cmd, env=env)
 
 
+class StepLoop:
+    """The bench's step sequence.  Step k runs decoder k % D inside stream context k % D (a factory:
+    torch.cuda.stream of that decoder's stream on the GPU; contextlib.nullcontext on the CPU), then -- with a
+    gatherer (N > 1 or --gather) -- packs and issues that step's decode exchange on the same stream,
+    with no host sync.  Kept steps' exchanges are resolved after the loop, in issue order: they are
+    collectives, so every rank issues and resolves them in the same order (tests/test_distributed_gloo.py
+    drives this loop at world size 2 with fake decoders)."""
+
+    def __init__(self, decs, stream_ctxs, x, gatherer=None):
+        self.decs, self.ctxs, self.x, self.gatherer = decs, stream_ctxs, x, gatherer
+        self.handles = []
+
+    def step(self, k, keep=False, ev=None):
+        D = len(self.decs)
+        with self.ctxs[k % D]():
+            out, counts = self.decs[k % D].run(self.x)
+            if self.gatherer is not None:
+                h = self.gatherer.start(out, counts)
+                if keep:
+                    self.handles.append(h)   # every timed step's exchange is resolved after the loop
+            if ev is not None:
+                ev.record()                  # on this step's stream, after its work
+        return counts
+
+    def resolve(self):
+        """Resolve every kept exchange in issue order -> [(records, counts, totals, capacity)]."""
+        out = []
+        for h in self.handles:
+            out.append((*h.resolve(), h.capacity))
+        self.handles.clear()
+        return out
+
+
 LINE_MAX = 4096   # bytes of the stdout line; the driver's parser gave up on the 23.8 KB r05 line
 
 
@@ -1310,18 +1343,8 @@ def main():
     # step's exchange is resolved after the timed loop.  Records carry global slot ids.
     exchange = world > 1 or args.gather
     gatherer = DecodeGatherer(S, dec.cap, slot_offset=rank * S) if exchange else None
-    handles = []
-
-    def step(k, keep=False, ev=None):
-        with torch.cuda.stream(streams[k % D]):
-            out, counts = decs[k % D].run(x)
-            if exchange:
-                h = gatherer.start(out, counts)
-                if keep:
-                    handles.append(h)   # every timed step's exchange is resolved after the loop
-            if ev is not None:
-                ev.record()             # on this step's stream, after its work
-        return counts
+    loop = StepLoop(decs, [lambda st_=st_: torch.cuda.stream(st_) for st_ in streams], x, gatherer)
+    step = loop.step
 
     # clock settling before the W warmup steps: k_bp's shader clock ramps over its first launches
     # (step_times of the driver's --warmup 5 lines: the first timed pairs 10 % slower than the last),
@@ -1353,7 +1376,8 @@ def main():
             if done_:
                 break
             prev = t_
-    for k_ in range(max(args.warmup, D)):
+    n_warm = max(args.warmup, D)
+    for k_ in range(n_warm):
         step(k_)
     torch.cuda.synchronize()
     if world > 1:
@@ -1366,7 +1390,7 @@ def main():
     t0 = time.perf_counter()
     step_ev[0].record()
     for i_ in range(args.steps):
-        counts = step(i_, keep=True, ev=step_ev[i_ + 1])
+        counts = step(n_warm + i_, keep=True, ev=step_ev[i_ + 1])   # the alternation continues
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -1393,11 +1417,9 @@ def main():
         # resolve every timed step's exchange in issue order (collectives: all ranks do the same);
         # a step whose total exceeded the capacity runs its overflow exchange here and grows it
         over_steps = 0
-        for h in handles:
-            recs_g, cnts_g, totals_g = h.resolve()
-            over_steps += int(int(totals_g.max()) > h.capacity)
+        for recs_g, cnts_g, totals_g, cap_ in loop.resolve():
+            over_steps += int(int(totals_g.max()) > cap_)
         gather_last = (gathered_records(recs_g, totals_g), cnts_g.cpu().numpy(), totals_g.cpu().tolist())
-        handles.clear()
         gather = {"backend": dist.get_backend(), "world": world,
                   "rows_per_rank_sent": rows_sent, "bytes_per_rank_sent": pack_bytes(gatherer.S_pad, rows_sent),
                   "decodes_per_rank_last_step": gather_last[2], "steps_over_capacity": over_steps,

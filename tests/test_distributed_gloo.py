@@ -149,3 +149,89 @@ def test_gloo_world2_uneven_shards():
             assert tot == [10, 6]
             assert slots == want_slots and rows == want_rows
         assert res[2] == (4, 20, [10, 6])  # capacity min(S_pad * cap, max(64, 4 S_pad))
+
+
+class _FakeDecoder:
+    """Stands in for SlotDecoder in bench.StepLoop on the CPU: every run() returns a fresh record
+    buffer whose rows carry (rank, call number) in payload[0..1], and counts that vary per call, so
+    a gathered step shows which step of which rank it came from."""
+
+    def __init__(self, rank, lo, hi, cap, tag, log):
+        self.rank, self.lo, self.hi, self.cap, self.tag, self.log = rank, lo, hi, cap, tag, log
+
+    def run(self, x):
+        k = len(self.log)
+        self.log.append(self.tag)
+        n = self.hi - self.lo
+        counts = (torch.arange(n, dtype=torch.int32) + k + self.rank) % 3
+        rec = torch.zeros(n * self.cap * 40, dtype=torch.uint8)
+        v = rec.view(n, self.cap, 40)
+        v[:, :, 28] = self.rank
+        v[:, :, 29] = k
+        v.view(n, self.cap, 10, 4)[:, :, 2, :] = torch.arange(n, dtype=torch.int32)[:, None].view(torch.uint8)[:, None, :]
+        return rec, counts
+
+
+def _steploop_worker(rank, world, port, S, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        try:
+            import contextlib
+            import importlib.util
+            root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+            spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(root, "bench.py"))
+            bench = importlib.util.module_from_spec(spec)
+            spec.loader.exec_module(bench)
+            from ft8_demodulator_amd.distributed import DecodeGatherer, gathered_records
+            cap, D, K = 4, 2, 6
+            log = []
+            decs = [_FakeDecoder(rank, rank * S, (rank + 1) * S, cap, d, log) for d in range(D)]
+            # a small capacity so some steps overflow it and resolve() runs the second exchange
+            g = DecodeGatherer(S, cap, slot_offset=rank * S, capacity=4)
+            loop = bench.StepLoop(decs, [contextlib.nullcontext] * D, None, g)
+            for k in range(3):              # warm-up steps: their exchanges are issued, not kept
+                loop.step(k)
+            for k in range(3, 3 + K):       # the timed steps, kept; the alternation continues
+                loop.step(k, keep=True)
+            res = loop.resolve()
+            out = []
+            for i, (recs, cnts, tot, capacity) in enumerate(res):
+                flat = gathered_records(recs, tot)
+                call = 3 + i                # every rank's call number of this timed step
+                ok = bench.gather_check(flat, cnts.numpy(), tot.tolist(), S, world, int(tot.sum()), cap)
+                tags = sorted(set(zip(flat["payload"][:, 0].tolist(), flat["payload"][:, 1].tolist())))
+                out.append((ok["gather_ok"], tags, call, int(tot.max()) > capacity))
+            q.put((rank, log, out, g.grown))
+        except Exception as e:  # noqa: BLE001
+            q.put((rank, "error " + repr(e), None, None))
+            raise
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_bench_step_loop_depth2():
+    """bench.StepLoop at world size 2 over gloo, depth 2: the steps alternate over the two decoders,
+    every warm-up and timed step issues its exchange without resolving it, the kept exchanges are
+    resolved after the loop in issue order -- each gathered step holds exactly that step's records
+    from both ranks (a rank resolving out of order would pair step k of one rank with another step
+    of the other), gather_ok holds for every step, and overflowing steps take the second exchange."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 33500 + (os.getpid() % 2000)
+    ps = [ctx.Process(target=_steploop_worker, args=(r, 2, port, 5, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    out = sorted([q.get(timeout=180) for _ in ps], key=lambda o: o[0])
+    for p in ps:
+        p.join(timeout=60)
+    assert all(not isinstance(o[1], str) for o in out), out
+    for rank, log, steps, grown in out:
+        assert log == [k % 2 for k in range(9)]                   # decoder k % D ran step k
+        assert len(steps) == 6
+        for ok, tags, call, over in steps:
+            assert ok
+            assert tags == [(r, call) for r in range(2)]            # both ranks' records of this very step
+        assert any(over for *_, over in steps) and grown >= 1      # the overflow exchange ran
+    assert out[0][2] == out[1][2]

@@ -13,7 +13,7 @@ KERNELS = ("ft8::k_stft3840p<float, true>", "ft8::k_score2<2, 2, true>", "ft8::k
 DUR = (150, 220, 30, 80, 1500, 5)  # us
 
 
-def _write(tmp, steps, depth, warmup, K, settle=None):
+def _write(tmp, steps, depth, warmup, K, settle=None, compact=False):
     """steps: list of (stream, t0_us) -> trace csv + bench line."""
     rows, did = [], 0
     for sid, t0 in steps:
@@ -33,6 +33,13 @@ def _write(tmp, steps, depth, warmup, K, settle=None):
             "stages_ms": {"stft": 0.15, "score": 0.22, "select": 0.03, "llr": 0.08, "bp": 1.5, "compact": 0.005}}
     if settle is not None:
         line["settle"] = {"steps": settle, "block_ms": [], "max_steps": 96}
+    if compact:
+        # round 6's stdout line: settle_steps inline, stages_ms only in the legs file it names
+        with open(os.path.join(tmp, "legs.json"), "w") as f:
+            json.dump(line, f)
+        line = {k: line[k] for k in ("warmup", "steps", "ms_per_step", "depth", "roofline")}
+        line["settle_steps"] = settle or 0
+        line["legs"] = "gpurun_out/legs.json"   # resolved next to the line file when not found as given
     lf = os.path.join(tmp, "line.log")
     with open(lf, "w") as f:
         f.write(json.dumps(line) + "\n")
@@ -77,3 +84,20 @@ def test_settle_steps_precede_the_warmup(tmp_path):
     d = _write(str(tmp_path), steps, depth=1, warmup=W, K=K, settle=S)
     assert d["warmup"] == S + W and d["timed_steps"] == K and d["decode_steps_found"] == S + W + K
     assert abs(d["timed_period_ms_mean"] - step / 1000) < 1e-9
+
+
+def test_compact_line_with_legs_file(tmp_path):
+    """The compact stdout line (settle_steps inline, stages_ms in the legs file it names) gives the
+    same reconciliation as the full line; depth-2 per-kernel means are labelled overlap-inflated."""
+    step = sum(DUR)
+    S, W, K = 8, 3, 4
+    steps = [(0, i * 3000) for i in range(S)] + [(0, S * 3000 + i * step) for i in range(W + K)]
+    d = _write(str(tmp_path), steps, depth=1, warmup=W, K=K, settle=S, compact=True)
+    assert d["warmup"] == S + W and d["timed_steps"] == K
+    assert "line_stage_vs_trace_timed" in d and abs(d["line_stage_vs_trace_timed"]["bp"] - 1.0) < 1e-9
+    period = 1800
+    steps = [(1 + (i % 2), i * period) for i in range(5 + 6)]
+    t = 11 * period + step
+    steps += [(0, t + i * step) for i in range(6)]
+    d = _write(str(tmp_path), steps, depth=2, warmup=5, K=6, compact=True)
+    assert "OVERLAP-INFLATED" in d["timed_kernels_note"]

@@ -14,6 +14,7 @@ against the profiler's own clock.
 import argparse
 import csv
 import json
+import os
 import statistics as st
 
 STEP = ("k_stft", "k_score", "k_select", "k_llr", "k_bp", "k_compact")
@@ -35,9 +36,18 @@ def main():
     a = ap.parse_args()
     with open(a.line) as f:
         line = next(json.loads(l) for l in f if l.startswith("{"))
+    # round 6: the stdout line is compact; the full record (stages_ms, settle, ...) is in its legs file
+    legs = line.get("legs")
+    if legs:
+        base = os.path.dirname(os.path.abspath(a.line))
+        for cand in (legs, os.path.join(base, os.path.basename(legs))):
+            if os.path.exists(cand):
+                with open(cand) as f:
+                    line = {**json.load(f), **{k: v for k, v in line.items() if k not in ("roofline", "depth")}}
+                break
     depth = int(line.get("depth", {}).get("contexts", 1) or 1)
     # steps before the timed loop: the clock-settle phase's (bench `settle`, round 5), then the warmup
-    settle = int((line.get("settle") or {}).get("steps", 0) or 0)
+    settle = int(line.get("settle_steps", (line.get("settle") or {}).get("steps", 0)) or 0)
     W = settle + max(line["warmup"], depth) if a.warmup is None else a.warmup
     K = line["steps"]
     rows = []
@@ -89,6 +99,10 @@ def main():
         "timed_span_ms_mean": st.mean(p["span_ms"] for p in per) if per else None,
         "timed_period_ms_mean": loop_ms / len(timed) if timed else None,
         "timed_kernels_ms_mean": {k: st.mean(p["kernels_ms"][k] for p in per) for k in per[0]["kernels_ms"]} if per else {},
+        "timed_kernels_note": ("depth 1: per-kernel durations of the timed steps" if depth == 1 else
+                               f"depth {depth}: OVERLAP-INFLATED start->end spans of kernels whose steps overlap "
+                               "(they include time spent waiting for CUs the other stream holds) -- not per-kernel "
+                               "costs; use one_chain_kernels_ms_mean for those"),
         "k_bp_in_steps_ms": bp_step, "k_bp_replays_ms": bp_replay,
         "k_bp_replay_mean_ms": st.mean(bp_replay) if bp_replay else None,
         "k_bp_timed_mean_ms": st.mean(p["kernels_ms"]["k_bp"] for p in per) if per else None,
