@@ -21,6 +21,7 @@
 //            summed in record order (deterministic).
 // k_merge    one wave per slot: pass-2 records with a payload not decoded in pass 1 are appended.
 #include <algorithm>
+#include <mutex>
 #include <type_traits>
 
 #include "tx_device.h"
@@ -607,10 +608,28 @@ size_t sub_est_bytes() { return sizeof(SubEst); }
 
 // dynamic LDS above the default 64 KB needs the kernel's attribute raised first (the pulse table is
 // nsps float4s: 61.4 KB at 24 kHz, more above)
+// The attribute is set once per kernel instantiation and device, and again only when a launch needs
+// more than any before it (it was a host-side call per launch); static + dynamic LDS is
+// compared against the 64 KB default, the kernel's static size queried once.
 template <typename K>
 static hipError_t allow_lds(K kern, size_t dyn) {
-  if (dyn <= 32 * 1024) return hipSuccess;  // + static LDS: stay clear of the 64 KB default
-  return hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
+  constexpr int kMaxDev = 64;
+  static std::mutex mu;
+  static size_t static_lds[kMaxDev];
+  static size_t granted[kMaxDev];
+  static bool queried[kMaxDev];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) dev = 0;
+  std::lock_guard<std::mutex> lk(mu);
+  if (!queried[dev]) {
+    hipFuncAttributes fa{};
+    static_lds[dev] = hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(kern)) == hipSuccess ? fa.sharedSizeBytes : 0;
+    queried[dev] = true;
+  }
+  if (static_lds[dev] + dyn <= 64 * 1024 || dyn <= granted[dev]) return hipSuccess;
+  const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
+  if (e == hipSuccess) granted[dev] = dyn;
+  return e;
 }
 
 hipError_t launch_sub_est(const SubLaunch& a, hipStream_t s) {

@@ -29,7 +29,15 @@ from ._pipeline import SlotDecoder, records_to_results, warn_truncated
 
 class StreamDecoder:
     """Host -> device upload on a copy stream overlapped with ft8_decode_batch on `depth` decoders
-    (own context and compute stream each; depth 1 = one decoder on the current stream)."""
+    (own context and compute stream each; depth 1 = one decoder on the current stream).
+
+    Memory: depth + 2 device and depth + 2 pinned host sample buffers of max_batch x n_samples
+    (int16 PCM: 2 B per sample; float32: 4 B), plus depth + 2 pinned result buffers, plus one library
+    context per decoder beyond the first (its own scratch: waterfall, scores, LLRs of max_batch
+    slots).  At max_batch 256 and 180 000 int16 samples a sample buffer is 92 MB, so the default
+    depth 2 holds 4 x 92 MB on the device and 4 x 92 MB pinned, against 3 x 92 MB each at depth 1,
+    and creates one extra context (~0.5 GB of decode scratch at 256 slots).  Choose depth 1 for one
+    or two batches: there is nothing to overlap."""
 
     def __init__(self, n_samples: int, sample_rate: int = 12000, max_batch: int = 256, pcm16: bool = True,
                  device=None, depth: int = 2, **decoder_kw):
@@ -185,8 +193,10 @@ class StreamDecoder:
             yield done
 
 
-def decode_wave_files(paths: List[str], batch: int = 256, device=None, **decoder_kw) -> List[list]:
-    """Decode many 16-bit PCM WAV files of one sample rate and length -> results per file."""
+def decode_wave_files(paths: List[str], batch: int = 256, device=None, depth=None, **decoder_kw) -> List[list]:
+    """Decode many 16-bit PCM WAV files of one sample rate and length -> results per file.
+    depth: StreamDecoder's; by default 2 when there are more than two batches (upload and decodes
+    overlap), else 1 (no second context, fewer buffers)."""
     from .from_wave import _read_raw
     if not paths:
         return []
@@ -205,7 +215,11 @@ def decode_wave_files(paths: List[str], batch: int = 256, device=None, **decoder
                 arr[j] = d
             yield arr
 
-    sd = StreamDecoder(n, sample_rate=fs, max_batch=min(batch, len(paths)), pcm16=True, device=device, **decoder_kw)
+    n_batches = -(-len(paths) // batch)
+    if depth is None:
+        depth = 2 if n_batches > 2 else 1
+    sd = StreamDecoder(n, sample_rate=fs, max_batch=min(batch, len(paths)), pcm16=True, device=device,
+                       depth=depth, **decoder_kw)
     out: List[list] = []
     for res in sd.decode_batches(batches()):
         out.extend(res)

@@ -18,6 +18,9 @@
  *     ordered across streams by the library: an entry point that uses the context's scratch, called
  *     on a stream other than the previous such call's, waits (device side) for that call's work, so
  *     two streams sharing one context serialise; independent streams want one context each.
+ *     Every such call moves the context's order to its stream -- also one that enqueued nothing
+ *     (n_slots = 0) or failed its argument checks: the next call on another stream then waits for
+ *     whatever that stream holds at that point (a false dependency, never a missing one).
  */
 #ifndef FT8HIP_H
 #define FT8HIP_H

@@ -203,6 +203,33 @@ def test_stream_decoder_matches_resident_decode(gpu):
             got.extend(res)
         assert key(got) == key(ref), depth
     assert sum(len(r) for r in got) > 0
+    # buffer recycling: at least 2 (depth + 2) batches so every device, pinned-input and
+    # pinned-output buffer is reused (and decode_batches' start-next-upload-before-waiting path
+    # runs on reused buffers), ragged last batch; then borrow=True with the caller cycling through
+    # depth + 3 pinned buffers and rewriting each right after its batch's results are yielded
+    for depth in (2, 3):
+        sd = StreamDecoder(pcm.shape[1], max_batch=2, depth=depth, **kw)
+        nb = 2 * (depth + 2) + 1
+        order = [(3 * j) % 24 for j in range(nb * 2)]          # slots in a permuted order
+        chunks = [pcm[order[2 * j:2 * j + 2]] for j in range(nb - 1)] + [pcm[order[2 * nb - 2:2 * nb - 1]]]
+        got = []
+        for res in sd.decode_batches(chunks):
+            got.extend(res)
+        exp = [ref[s] for c in range(nb) for s in order[2 * c:2 * c + (2 if c < nb - 1 else 1)]]
+        assert key(got) == key(exp), depth
+        ring = [torch.empty((2, pcm.shape[1]), dtype=torch.int16).pin_memory() for _ in range(depth + 3)]
+
+        def lent():
+            for j, c in enumerate(chunks):
+                buf = ring[j % len(ring)]
+                buf[:c.shape[0]].copy_(torch.from_numpy(c))
+                yield buf[:c.shape[0]]
+
+        got = []
+        for j, res in enumerate(sd.decode_batches(lent(), borrow=True)):
+            got.extend(res)
+            ring[j % len(ring)].fill_(0)     # the caller rewrites a buffer once its results are back
+        assert key(got) == key(exp), ("borrow", depth)
     from ft8_demodulator_amd import decode_ft8_from_wave
     wavs = [os.path.join(DATA, n) for n in ("synth_cfg1.wav", "synth_cfg2.wav")]
     files = decode_wave_files(wavs, batch=2)

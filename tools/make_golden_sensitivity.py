@@ -8,7 +8,8 @@ reach the same per-slot verdicts (tests/test_gpu_harness.py::test_gpu_sensitivit
 This checks BASELINE.md section 1's table (snr_vs_freq_analysis.xlsx: -9 dB at B = 1 000 Hz, -13 dB at
 B = 3 000 Hz) against the committed harness and decoder: the success ratio per point is stored.
 
-Usage:  cd /tmp && python /root/repo/tools/make_golden_sensitivity.py
+Usage:  cd /tmp && python /root/repo/tools/make_golden_sensitivity.py [extend]
+        (extend: add only the rates not yet in tests/golden/sensitivity_ref.json)
 """
 import json
 import os
@@ -20,7 +21,10 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import make_golden_harness as MH  # noqa: E402  (reference import recipe, harness_input, KW)
 
-POINTS = {2000: (-14.0, -13.0, -12.0, -11.0, -10.0), 6000: (-20.0, -19.0, -18.0, -17.0, -16.0, -15.0, -14.0)}
+POINTS = {2000: (-14.0, -13.0, -12.0, -11.0, -10.0), 6000: (-20.0, -19.0, -18.0, -17.0, -16.0, -15.0, -14.0),
+          # round 6: a chirp-z rate (nfft 1760 = 2^5 * 5 * 11) and one >= 9 kHz, around the GPU table's
+          # thresholds (-18.2 dB at 5 500 Hz, -20.6 dB at 10 000 Hz)
+          5500: (-19.5, -19.0, -18.5, -18.0, -17.5), 10000: (-21.5, -21.0, -20.5, -20.0, -19.5)}
 ROUNDS = 20
 SEED0 = 70000
 
@@ -30,7 +34,17 @@ def main():
     os.chdir(tempfile.mkdtemp(prefix="ft8gold_"))
     out = {"rounds": ROUNDS, "kwargs": MH.KW, "points": []}
     seed = SEED0
+    path = os.path.join(MH.GOLD, "sensitivity_ref.json")
+    done = set()
+    if sys.argv[1:] == ["extend"]:
+        # keep the rates already stored (and their seeds); add the others, seeds continuing after
+        with open(path) as f:
+            out = json.load(f)
+        done = {p["fs"] for p in out["points"]}
+        seed = max(s_ for p in out["points"] for s_ in p["seeds"]) + 1
     for fs, snrs in POINTS.items():
+        if fs in done:
+            continue
         for snr in snrs:
             t0 = time.time()
             seeds, ok = [], []
@@ -43,7 +57,7 @@ def main():
             out["points"].append({"fs": fs, "snr_db": snr, "seeds": seeds, "success": ok,
                                   "ratio": sum(ok) / ROUNDS})
             print(fs, snr, sum(ok), "/", ROUNDS, round(time.time() - t0, 1), "s", flush=True)
-    with open(os.path.join(MH.GOLD, "sensitivity_ref.json"), "w") as f:
+    with open(path, "w") as f:
         json.dump(out, f, indent=1)
     print("wrote", os.path.join(MH.GOLD, "sensitivity_ref.json"))
 
