@@ -604,7 +604,7 @@ int do_sync_select(ft8_ctx* c, const void* d_wf, int wf_f64, int n_slots, int T,
   }
   if ((rc = ensure(c, c->smask, sizeof(uint64_t) * (size_t)n_slots * smask_words(g)))) return rc;
   if ((rc = ensure(c, c->warn, sizeof(int32_t) * (size_t)n_slots))) return rc;
-  if ((rc = ensure(c, c->rowsum, sizeof(RowSummary) * (size_t)n_slots * g.NT))) return rc;
+  if ((rc = ensure(c, c->rowsum, sizeof(RowSummary) * (size_t)n_slots * g.NT * n_segments(g.NF)))) return rc;
   // float32 scores: k_select leaves equal scores in scan order and k_tie_apply replays the
   // reference heap for the slots that have them (the same code k_llr runs inside decode_batch)
   int32_t* tie = nullptr;
@@ -625,7 +625,7 @@ int do_sync_select(ft8_ctx* c, const void* d_wf, int wf_f64, int n_slots, int T,
 }
 
 // score + select on caller-provided scratch (scores [n_slots][score_elems], smask
-// [n_slots][smask_words], warn [n_slots], rowsum [n_slots][NT]); compact: the score kernel may
+// [n_slots][smask_words], warn [n_slots], rowsum [n_slots][NT][nseg]); compact: the score kernel may
 // write only the passing scores (k_score2 path, reference selection), else the full grid
 int sync_select_core(ft8_ctx* c, const void* d_wf, int wf_f64, int n_slots, int T, int F, const ft8_params* p,
                      int32_t* cand, double* cand_score, int32_t* cand_count, void* scores, uint64_t* smask,
@@ -719,7 +719,7 @@ int decode_pass(ft8_ctx* c, const void* d_samples, int dtype, int64_t n_samples,
     if ((rc = sync_select_core(c, wf, f64, ns, T, F, p, cand, cand_score, cand_count,
                                (char*)c->scores.p + esz * (size_t)c0 * score_elems(gr),
                                (uint64_t*)c->smask.p + (size_t)c0 * smask_words(gr), 1, (int32_t*)c->warn.p + c0,
-                               (RowSummary*)c->rowsum.p + (size_t)c0 * gr.NT, cs, tie)))
+                               (RowSummary*)c->rowsum.p + (size_t)c0 * gr.NT * n_segments(gr.NF), cs, tie)))
       return rc;
     BpLaunch B{};
     B.wf = wf;
@@ -1266,7 +1266,7 @@ int ft8_decode_batch(ft8_ctx* c, const void* d_samples, int dtype, int64_t n_sam
   if ((rc = ensure(c, c->scores, esz * (size_t)n_slots * score_elems(gr)))) return rc;
   if ((rc = ensure(c, c->smask, sizeof(uint64_t) * (size_t)n_slots * smask_words(gr)))) return rc;
   if ((rc = ensure(c, c->warn, sizeof(int32_t) * (size_t)n_slots))) return rc;
-  if ((rc = ensure(c, c->rowsum, sizeof(RowSummary) * (size_t)n_slots * gr.NT))) return rc;
+  if ((rc = ensure(c, c->rowsum, sizeof(RowSummary) * (size_t)n_slots * gr.NT * n_segments(gr.NF)))) return rc;
   if (!f64 && (rc = ensure(c, c->tie, sizeof(int32_t) * (size_t)n_slots * tie_stride(N)))) return rc;
   if (p->steps_per_symbol <= 0 || p->bins_per_tone <= 0) return fail(c, FT8_E_ARG, "bad oversampling factors");
   if (p->flags & ~(FT8_FLAG_TOPK | FT8_FLAG_SUBTRACT)) return fail(c, FT8_E_ARG, "unknown bits in ft8_params.flags");

@@ -158,7 +158,8 @@ struct SyncLaunch {
   int32_t* warn;           // scratch [n_slots] (bit 0: tie reached a heap comparison,
                            //                    bit 2: equal scores in the selected set,
                            //                    bit 3: their order deferred to the LLR kernel)
-  RowSummary* rowsum;      // scratch [n_slots][NT]: passing count + max passing score per time row
+  RowSummary* rowsum;      // scratch [n_slots][NT][n_segments(NF)]: passing count + max passing score
+                           // per (time row, 128-column segment)
   int32_t* tie = nullptr;  // nullable scratch [n_slots][tie_stride(N)]: defer the order of equal
                            // scores to the LLR kernel (warn bit 3); k_compact applies it
   int topk = 0;            // FT8_FLAG_TOPK: k_topk instead of the reference heap selection

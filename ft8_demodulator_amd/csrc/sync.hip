@@ -93,7 +93,7 @@ __global__ __launch_bounds__(kScoreThreads) void k_score(ScoreArgs a) {
   constexpr int kGroups = kScoreThreads / TW;
   const int af = c0 + lane_col;
   T* out = reinterpret_cast<T*>(a.scores) + (int64_t)slot * a.NT * a.NF;
-  RowSummary* rs = a.rowsum + (int64_t)slot * a.NT;
+  RowSummary* rs = a.rowsum + (int64_t)slot * a.NT * a.nseg;
   const int sps = a.sps, bpt = a.bpt, nb = a.num_blocks;
   for (int ti = rgroup; ti < a.NT; ti += kGroups) {
     if (af >= a.NF) continue;
@@ -123,8 +123,9 @@ __global__ __launch_bounds__(kScoreThreads) void k_score(ScoreArgs a) {
     else res = score / (T)n;
     out[(int64_t)ti * a.NF + af] = res;
     if (passes(res, a.min_score, a.cmp_f64)) {
-      atomicAdd(&rs[ti].count, 1u);
-      atomicMax(&rs[ti].maxkey, order_key((double)res));
+      RowSummary* e = rs + (int64_t)ti * a.nseg + af / kSegCols;
+      atomicAdd(&e->count, 1u);
+      atomicMax(&e->maxkey, order_key((double)res));
       const int c = af % kSegCols;
       atomicOr(reinterpret_cast<unsigned long long*>(
                    &a.smask[(((int64_t)slot * a.NT + ti) * a.nseg + af / kSegCols) * 2 + (c & 1)]),
@@ -353,7 +354,7 @@ __global__ __launch_bounds__(kS2Threads) void k_score2(ScoreArgs a) {
   }
 
   float* out = reinterpret_cast<float*>(a.scores) + (COMPACT ? 0 : (int64_t)slot * a.NT * a.NF);
-  RowSummary* rs = a.rowsum + (int64_t)slot * a.NT;
+  RowSummary* rs = a.rowsum + (int64_t)slot * a.NT * a.nseg;
 #pragma unroll
   for (int u = 0; u < kS2Rows; ++u) {
     const int j = w + u * kS2Waves;
@@ -384,15 +385,22 @@ __global__ __launch_bounds__(kS2Threads) void k_score2(ScoreArgs a) {
       if (v1) orow[af + 1] = res[1];
     }
     if (lane == 0) *reinterpret_cast<ulonglong2*>(a.smask + 2 * seg) = make_ulonglong2(b0, b1);
+    // the (row, segment) summary: this wave is the segment's only writer, so a plain store (every
+    // entry written, none skipped: no memset, no atomics)
     const unsigned cnt = (unsigned)(__popcll(b0) + __popcll(b1));
+    unsigned long long key = 0ull;
     if (cnt) {
       float mx = p0 ? res[0] : -INFINITY;
       if (p1) mx = fmaxf(mx, res[1]);
       mx = wave_max(mx);
-      if (lane == 0) {
-        atomicAdd(&rs[ti].count, cnt);
-        atomicMax(&rs[ti].maxkey, order_key((double)mx));
-      }
+      key = order_key((double)mx);
+    }
+    if (lane == 0) {
+      RowSummary e;
+      e.count = cnt;
+      e.pad = 0;
+      e.maxkey = key;
+      rs[seg - (int64_t)slot * a.NT * a.nseg] = e;
     }
   }
 }
@@ -447,8 +455,7 @@ hipError_t launch_score_t(const SyncLaunch& L, hipStream_t s) {
   a.min_score = L.min_score;
   a.cmp_f64 = L.min_score_f64;
   a.n_slots = L.n_slots;
-  hipError_t e = hipMemsetAsync(L.rowsum, 0, sizeof(RowSummary) * (size_t)L.n_slots * L.NT, s);
-  if (e != hipSuccess) return e;
+  hipError_t e = hipSuccess;
   if constexpr (sizeof(T) == 4) {
     if (score2_path(L)) {
       switch (L.bpt) {
@@ -461,8 +468,11 @@ hipError_t launch_score_t(const SyncLaunch& L, hipStream_t s) {
       }
     }
   }
-  // k_score sets the mask bits of its passing candidates one by one
+  // k_score sets the mask bits and the (row, segment) summaries of its passing candidates one by one
+  // (k_score2 writes every entry of both: no memset on its path)
   e = hipMemsetAsync(L.smask, 0, sizeof(uint64_t) * 2 * (size_t)L.n_slots * L.NT * a.nseg, s);
+  if (e != hipSuccess) return e;
+  e = hipMemsetAsync(L.rowsum, 0, sizeof(RowSummary) * (size_t)L.n_slots * L.NT * a.nseg, s);
   if (e != hipSuccess) return e;
   // rows touched by the grid: [t0 - sps, t0 + NT - 1 + 79 sps], clipped to the waterfall
   a.rlo = max(0, L.t0 - L.sps);
@@ -684,7 +694,19 @@ __global__ __launch_bounds__(kSelThreads) void k_select(SelectArgs a) {
     const int row = sg / nseg;
     return reinterpret_cast<const T*>(a.scores)[(int64_t)slot * a.total + (int64_t)row * a.NF + c];
   };
-  const RowSummary* rsum = a.rowsum + (int64_t)slot * a.NT;
+  const RowSummary* rsum = a.rowsum + (int64_t)slot * a.NT * nseg;
+  // a row's summary: its segments' passing counts added, their largest keys maxed
+  auto row_count_key = [&](int r, int* cnt, unsigned long long* key) {
+    int c_ = 0;
+    unsigned long long k_ = 0ull;
+    for (int sg = 0; sg < nseg; ++sg) {
+      const RowSummary e = rsum[(int64_t)r * nseg + sg];
+      c_ += (int)e.count;
+      k_ = e.maxkey > k_ ? e.maxkey : k_;
+    }
+    *cnt = c_;
+    *key = k_;
+  };
   const int N = a.N;
 
   // ---- row summaries: total passing, rows holding ranks < N, first row of the global maximum
@@ -693,8 +715,9 @@ __global__ __launch_bounds__(kSelThreads) void k_select(SelectArgs a) {
   unsigned long long gkey = 0;
   for (int r0 = 0; r0 < a.NT; r0 += kSelThreads) {
     const int r = r0 + threadIdx.x;
-    const int cnt = r < a.NT ? (int)rsum[r].count : 0;
-    const unsigned long long key = r < a.NT ? rsum[r].maxkey : 0ull;
+    int cnt = 0;
+    unsigned long long key = 0ull;
+    if (r < a.NT) row_count_key(r, &cnt, &key);
     int ctot;
     const int ex = total_pass + block_excl_sum(cnt, s_isum, &ctot);
     if (cnt > 0 && ex < N && ex + cnt >= N) s_flag[4] = r + 1;  // exactly one row holds rank N-1
@@ -705,7 +728,8 @@ __global__ __launch_bounds__(kSelThreads) void k_select(SelectArgs a) {
   __syncthreads();
   if (gkey != 0)
     for (int r = threadIdx.x; r < a.NT; r += kSelThreads)
-      if (rsum[r].maxkey == gkey) atomicMin(&s_flag[5], r);
+      for (int sg = 0; sg < nseg; ++sg)
+        if (rsum[(int64_t)r * nseg + sg].maxkey == gkey) { atomicMin(&s_flag[5], r); break; }
   __syncthreads();
   const int r_end = s_flag[4];   // rows [0, r_end) hold every rank < N
   const int g_row = s_flag[5];   // first row holding the global maximum (NT if nothing passes)
