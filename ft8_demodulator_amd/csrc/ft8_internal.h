@@ -2,6 +2,7 @@
 // kernel translation units (stft.hip, sync.hip, bp.hip) and the C-ABI (capi.hip).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <cstddef>
 #include <stdint.h>
 
 #include "../../include/ft8hip.h"
@@ -128,6 +129,7 @@ struct RowSummary {
   unsigned pad;
   unsigned long long maxkey;
 };
+static_assert(sizeof(RowSummary) == 16 && offsetof(RowSummary, maxkey) == 8, "k_select reads it as one uint4");
 __host__ __device__ inline unsigned long long order_key(double v) {
   union { double d; unsigned long long u; } x{v};
   return (x.u >> 63) ? ~x.u : (x.u | 0x8000000000000000ull);

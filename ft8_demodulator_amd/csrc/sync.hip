@@ -696,13 +696,22 @@ __global__ __launch_bounds__(kSelThreads) void k_select(SelectArgs a) {
   };
   const RowSummary* rsum = a.rowsum + (int64_t)slot * a.NT * nseg;
   // a row's summary: its segments' passing counts added, their largest keys maxed
+  // (16 segments' loads issued back to back: one round trip per row at the 12 kHz geometry's 15)
   auto row_count_key = [&](int r, int* cnt, unsigned long long* key) {
     int c_ = 0;
     unsigned long long k_ = 0ull;
-    for (int sg = 0; sg < nseg; ++sg) {
-      const RowSummary e = rsum[(int64_t)r * nseg + sg];
-      c_ += (int)e.count;
-      k_ = e.maxkey > k_ ? e.maxkey : k_;
+    const RowSummary* rr = rsum + (int64_t)r * nseg;
+    for (int s0 = 0; s0 < nseg; s0 += 16) {
+      uint4 e[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u)
+        e[u] = s0 + u < nseg ? *reinterpret_cast<const uint4*>(rr + s0 + u) : make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const unsigned long long k2 = ((unsigned long long)e[u].w << 32) | e[u].z;
+        c_ += (int)e[u].x;
+        k_ = k2 > k_ ? k2 : k_;
+      }
     }
     *cnt = c_;
     *key = k_;
@@ -712,12 +721,13 @@ __global__ __launch_bounds__(kSelThreads) void k_select(SelectArgs a) {
   // ---- row summaries: total passing, rows holding ranks < N, first row of the global maximum
   if (threadIdx.x == 0) { s_flag[4] = a.NT; s_flag[5] = a.NT; }
   int total_pass = 0;
-  unsigned long long gkey = 0;
+  unsigned long long gkey = 0, key0 = 0;
   for (int r0 = 0; r0 < a.NT; r0 += kSelThreads) {
     const int r = r0 + threadIdx.x;
     int cnt = 0;
     unsigned long long key = 0ull;
     if (r < a.NT) row_count_key(r, &cnt, &key);
+    if (r0 == 0) key0 = key;   // this thread's first row: the maximum search below reuses it
     int ctot;
     const int ex = total_pass + block_excl_sum(cnt, s_isum, &ctot);
     if (cnt > 0 && ex < N && ex + cnt >= N) s_flag[4] = r + 1;  // exactly one row holds rank N-1
@@ -727,9 +737,12 @@ __global__ __launch_bounds__(kSelThreads) void k_select(SelectArgs a) {
   }
   __syncthreads();
   if (gkey != 0)
-    for (int r = threadIdx.x; r < a.NT; r += kSelThreads)
-      for (int sg = 0; sg < nseg; ++sg)
-        if (rsum[(int64_t)r * nseg + sg].maxkey == gkey) { atomicMin(&s_flag[5], r); break; }
+    for (int r = threadIdx.x; r < a.NT; r += kSelThreads) {
+      int c_;
+      unsigned long long k_ = key0;
+      if (r >= kSelThreads) row_count_key(r, &c_, &k_);
+      if (k_ == gkey) atomicMin(&s_flag[5], r);
+    }
   __syncthreads();
   const int r_end = s_flag[4];   // rows [0, r_end) hold every rank < N
   const int g_row = s_flag[5];   // first row holding the global maximum (NT if nothing passes)
