@@ -705,7 +705,9 @@ __device__ __forceinline__ void atanh_group(double* v, int fast = 0) {
 #pragma unroll
   for (int i = 0; i < kDivGroup; ++i) {
     const double xv = v[i], x2 = xv * xv;
-    na[i] = xv * (945.0 + x2 * (-735.0 + x2 * 64.0));
+    // -735 + x2 * 64 as one fma: the product by 64 is exact (x2 is a finite square <= 1.02, or
+    // NaN), so RN(-735 + RN(64 x2)) == RN(-735 + 64 x2) bit for bit -- one VALU per edge less
+    na[i] = xv * (945.0 + x2 * __builtin_fma(x2, 64.0, -735.0));
     // -b/2 for b = 945 + x2 (-1050 + x2 225): every step is the reference's step scaled by -1/2,
     // exact (terms too small to scale exactly are absorbed by the constant they meet)
     nb[i] = (-472.5 + x2 * (525.0 + x2 * -112.5));
