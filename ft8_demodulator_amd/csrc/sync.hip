@@ -32,6 +32,8 @@
 // those; it sorts the set by score, and only when two selected scores are exactly equal (where
 // the reference's order depends on heap array positions) replays the reference's N heappushes
 // (one wave wide) to rebuild the heap array and reproduce its stable sort.
+#include <climits>
+
 #include "ft8_internal.h"
 #include "heap_replay.h"
 
@@ -231,18 +233,41 @@ __device__ __forceinline__ f32x2 ld2(const float* p) {
 // Costas band m of the tile (staged rows a0 - SPS + 36 m SPS + SPS u, u < H; columns [c0, c0 + P))
 // as float4 loads into registers; rows outside the waterfall / columns past F are zero and never
 // read by a valid candidate.  Thread t owns float4 t + 512 it.
+// The thread's part of that staging, computed once per workgroup: for each of its float4s the
+// band-0 row (a sentinel far below 0 when the float4 lies past the tile or past column F) and its
+// element offset row * F + col; band m adds 36 m SPS rows to both (round 6: the division by Q,
+// the row/column arithmetic and the 64-bit address were re-derived for every band).
 template <int BPT, int SPS>
-__device__ __forceinline__ void s2_load(const float* wf, int T, int F, int a0, int c0, int m,
-                                        float4 (&v)[S2Geom<BPT, SPS>::kIter]) {
+struct S2Stage {
+  int row0[S2Geom<BPT, SPS>::kIter];
+  int off0[S2Geom<BPT, SPS>::kIter];
+};
+template <int BPT, int SPS>
+__device__ __forceinline__ S2Stage<BPT, SPS> s2_stage(int F, int a0, int c0) {
   using G = S2Geom<BPT, SPS>;
+  S2Stage<BPT, SPS> st;
 #pragma unroll
   for (int it = 0; it < G::kIter; ++it) {
     const int idx = (int)threadIdx.x + it * kS2Threads;
     const int rw = idx / G::Q, q4 = idx - rw * G::Q;
-    const int row = a0 - SPS + 36 * m * SPS + SPS * rw, col = c0 + 4 * q4;
+    const int row = a0 - SPS + SPS * rw, col = c0 + 4 * q4;
+    const bool ok = idx < G::H * G::Q && col < F;
+    st.row0[it] = ok ? row : INT_MIN / 2;
+    st.off0[it] = row * F + col;   // slot waterfalls hold < 2^31 floats
+  }
+  return st;
+}
+template <int BPT, int SPS>
+__device__ __forceinline__ void s2_load(const float* wf, int T, int F, const S2Stage<BPT, SPS>& st, int m,
+                                        float4 (&v)[S2Geom<BPT, SPS>::kIter]) {
+  using G = S2Geom<BPT, SPS>;
+  const int drow = 36 * m * SPS;                  // wave-uniform
+  const float* wb = wf + (int64_t)drow * F;
+#pragma unroll
+  for (int it = 0; it < G::kIter; ++it) {
+    const int row = st.row0[it] + drow;
     v[it] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (idx < G::H * G::Q && row >= 0 && row < T && col < F)
-      v[it] = *reinterpret_cast<const float4*>(wf + (int64_t)row * F + col);
+    if ((unsigned)row < (unsigned)T) v[it] = *reinterpret_cast<const float4*>(wb + st.off0[it]);
   }
 }
 
@@ -293,7 +318,8 @@ __global__ __launch_bounds__(kS2Threads) void k_score2(ScoreArgs a) {
   }
 
   float4 v[G::kIter];
-  if (vec) s2_load<BPT, SPS>(wf, a.T, a.F, a0, c0, 0, v);
+  const S2Stage<BPT, SPS> stg = s2_stage<BPT, SPS>(a.F, a0, c0);
+  if (vec) s2_load<BPT, SPS>(wf, a.T, a.F, stg, 0, v);
 #pragma unroll 1
   for (int m = 0; m < 3; ++m) {
     if (m > 0) __syncthreads();  // every wave has scored band m - 1
@@ -303,7 +329,7 @@ __global__ __launch_bounds__(kS2Threads) void k_score2(ScoreArgs a) {
         const int idx = (int)threadIdx.x + it * kS2Threads;
         if (idx < G::H * G::Q) reinterpret_cast<float4*>(tile)[idx] = v[it];
       }
-      if (m < 2) s2_load<BPT, SPS>(wf, a.T, a.F, a0, c0, m + 1, v);  // in flight while band m is scored
+      if (m < 2) s2_load<BPT, SPS>(wf, a.T, a.F, stg, m + 1, v);  // in flight while band m is scored
     } else {
       for (int i = threadIdx.x; i < G::kFloats; i += kS2Threads) {
         const int rr = i / P, cc = i - rr * P;
