@@ -1235,6 +1235,9 @@ def main():
     ap.add_argument("--stage-steps", type=int, default=10, help="steps per single-stage event pass")
     ap.add_argument("--no-bp-stress", action="store_true", help="skip the config-4 BP stress leg")
     ap.add_argument("--no-h2d", action="store_true", help="skip the PCIe-inclusive streaming leg")
+    ap.add_argument("--no-single-call", action="store_true",
+                    help="skip the single-slot decode_ft8_message leg (its 1-slot k_bp launches would mix into a "
+                         "kernel-trace summary of the headline)")
     ap.add_argument("--no-subtract", action="store_true", help="skip the config-4 subtract-and-redecode leg")
     ap.add_argument("--subtract-oracle-slots", type=int, default=8,
                     help="slots of the subtract leg checked against oracle/subtract.py (0: none)")
@@ -1538,7 +1541,7 @@ def main():
     stream = None
     if world == 1 and not args.no_h2d:
         stream = h2d_stream(x, 40, kw, depth=D)
-    call = single_call(x) if world == 1 else None
+    call = single_call(x) if world == 1 and not args.no_single_call else None
     drift = None
     if world == 1 and not args.no_drift:
         drift = drift_correct(dev)

@@ -11,6 +11,9 @@
 #   bench            bench.py at its defaults
 #   driver           the driver's command: bench.py --gpus 1 --steps 20 --warmup 5
 #   prof             rocprofv3 --kernel-trace --stats of the headline workload (gpu_prof.sh)
+#   prof1            the same at --depth 1 without the single-call leg: every k_bp launch is one
+#                    un-overlapped 256-slot launch, so the --stats average is the line's launch_ms
+#   subprof          the config-4 subtract leg under a kernel trace + FETCH/WRITE/SQ passes (gpu_sub_prof.sh)
 #   rehearse=N       the N > 1 path with N ranks sharing cuda:0 over gloo (not a measurement)
 #   legs             bench.py with every side leg on (sensitivity included), legs file TAG_legs.json
 set -o pipefail
@@ -40,6 +43,8 @@ for st in "$@"; do
     driver) run driver 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 --legs-out gpurun_out/${T}_driver_legs.json \
               > gpurun_out/${T}_driver.json.log 2> gpurun_out/${T}_driver.err ;;
     prof) run prof 400 bash tools/gpu_prof.sh ${T} ;;
+    prof1) run prof1 400 bash tools/gpu_prof.sh ${T}_d1 --depth 1 --no-single-call ;;
+    subprof) run subprof 900 bash tools/gpu_sub_prof.sh ${T} ;;
     rehearse=*) n=${st#rehearse=}
         run rehearse 600 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 \
           --master-port 29533 bench.py --gpus $n --share-gpu --steps 10 --warmup 3 \
