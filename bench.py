@@ -1159,9 +1159,14 @@ def compact_line(full, legs_path):
                       if k in cfg}
     line["ldpc_candidates_per_s"] = full.get("ldpc_candidates_per_s")
     line["decodes_per_step"] = full.get("decodes_per_step")
+    iss = rf.get("issue") or {}
     line["roofline"] = {**_pick(rf, ("kernel", "bound", "achieved", "peak", "unit", "frac", "traffic",
                                      "traffic_source", "launch_ms", "flops_per_launch")),
-                        "clock_effective_ghz": clk.get("effective_ghz")}
+                        "clock_effective_ghz": clk.get("effective_ghz"),
+                        # the issue side of the bound (the committed SQ pass of this build): the exact
+                        # FP64 stream is ~0.5 of FLOP peak when the VALU is 100 % busy
+                        "valu_busy": iss.get("valu_busy_per_simd"),
+                        "valu_instructions_per_sweep": iss.get("valu_instructions_per_sweep")}
     line["roofline_hbm"] = _pick(rh, ("kernel", "bound", "achieved", "peak", "unit", "frac", "traffic",
                                       "launch_ms", "bytes_per_launch"))
     line["cpu_baseline"] = _pick(full.get("cpu_baseline"), ("value", "unit", "cores", "kind", "sample"))
