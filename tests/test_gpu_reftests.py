@@ -8,6 +8,9 @@
              bpt = sps = 4 (nfft 6400), K = 20, min_score 1
   ref_fs_frac  a non-integral sample rate, fs = 12006.3: nperseg 1921, nfft 3842 (chirp-z), computed
              on the float as spectrogram_analyse.py:32-34 does
+  bad_*      the production geometry (12 kHz, bpt = sps = 2, float32 samples: k_stft3840p, k_score2)
+             on a slot with a NaN burst, with +-inf samples, or with exact zeros at both ends
+             (-120 dB waterfall regions); NaN scores become -inf and NaN LLR vectors end BP at once
 
 Goldens from the reference itself (tools/make_golden_reftests.py -> tests/golden/reftests.*), inputs
 stored as the reference's float64 samples.  CPU tests pin the oracle (waterfall SHA-256, score-grid
@@ -36,7 +39,7 @@ def _sha(a):
 
 
 CASES = ("ref_noise", "ref_6k", "nochan_19db_s11", "nochan_17db_s12", "nochan_17db_s13", "nochan_15db_s14",
-         "ref_fs_frac")
+         "ref_fs_frac", "bad_nan_tail", "bad_inf_head", "bad_zero_half")
 
 
 @pytest.mark.parametrize("name", CASES)
@@ -56,8 +59,9 @@ def test_oracle_pinned_on_reference_test_geometry(reft, oracle, name):
     assert [[int(i // NF) + t0, int(i % NF)] for i in idx] == c["cands"]
     assert np.array_equal(np.asarray(sc, dtype=arr[f"{name}_scores"].dtype), arr[f"{name}_scores"])
     for j, (at, af) in enumerate(c["cands"][:len(arr[f"{name}_llr"])]):
+        # (bad_*: a candidate whose symbols touch a NaN frame has an all-NaN LLR vector)
         assert np.array_equal(oracle.llr(mag, kw["steps_per_symbol"], kw["bins_per_tone"], at, af),
-                              arr[f"{name}_llr"][j])
+                              arr[f"{name}_llr"][j], equal_nan=True)
     got = oracle.decode_ft8_message(x, c["fs"], **kw)
     exp = [(r["payload"], r["crc_calculated"], r["time_sec"], r["freq_hz"], r["score"]) for r in c["results"]]
     assert [(bytes(p).hex(), h, t, f, float(s)) for (p, h, _e, _ce, _cc, t, f, s) in got] == exp
@@ -82,7 +86,7 @@ def test_gpu_stages_on_reference_test_geometry(reft, oracle, gpu, name):
         v = np.zeros(174)
         ft8_extract_likelihood(wf, q, v)
         ftx_normalize_logl(v)
-        assert np.array_equal(v, arr[f"{name}_llr"][j]), j
+        assert np.array_equal(v, arr[f"{name}_llr"][j], equal_nan=True), j
     # every candidate's LLRs (GPU) through GPU BP == oracle BP, bit for bit
     from ft8_demodulator_amd import bp_decode
     for q in cands:

@@ -23,8 +23,16 @@ decode_ft8_message's results.
              bpt = sps = 2, -15 dB): the reference computes int(0.16 fs) = 1921 and int(fs / 6.25 * 2)
              = 3842 on the float (spectrogram_analyse.py:32-34)
 
-Usage:  cd /tmp && python /root/repo/tools/make_golden_reftests.py [nochannel]
-        (nochannel: add / replace only the nochan_* and ref_fs_frac cases in the existing files)
+  bad_*      non-finite and silent input at the production geometry (12 kHz, bpt = sps = 2, K = 40,
+             min_score 2, FLOAT32 samples as read_wave_file returns them): three signals (-12 / -10
+             / -8 dB full-band SNR) in unit noise with a NaN burst near the slot's end (bad_nan_tail),
+             +inf and -inf at its start (bad_inf_head), or exact zeros before the signals and after
+             them (bad_zero_half: a -120 dB waterfall there).  NaN frames make every score touching them NaN -> -inf
+             (ft8_decode.py:97-98) and every LLR vector touching them NaN after the normalisation,
+             which bp_decode ends at once (sum(plain) == 0)
+
+Usage:  cd /tmp && python /root/repo/tools/make_golden_reftests.py [nochannel | nonfinite]
+        (nochannel / nonfinite: add / replace only those cases in the existing files)
 """
 import contextlib
 import hashlib
@@ -142,15 +150,52 @@ def nochannel_cases(arrays):
     return out
 
 
+BAD = (("bad_nan_tail", 31), ("bad_inf_head", 32), ("bad_zero_half", 33))
+
+
+def nonfinite_cases(arrays):
+    """Three reference-generator signals in unit noise, float32, with the slot partly non-finite or
+    silent (module docstring)."""
+    out = []
+    fs, n = 12000, 180000
+    for name, seed in BAD:
+        np.random.seed(seed)
+        x = np.random.randn(n)
+        sent = []
+        for f0, snr_db in ((600.0, -12), (1350.0, -10), (2100.0, -8)):
+            p = np.random.randint(0, 255, size=10, dtype=np.uint8)
+            p[9] &= 0xF8
+            w = quiet(RG.ft8_generator, p, fs=fs, f0=f0, fc=0)
+            w = w * np.sqrt(10 ** (snr_db / 10) / np.mean(w ** 2))
+            m = min(n, len(w))
+            x[:m] += w[:m]
+            sent.append(p.tobytes().hex())
+        x = x.astype(np.float32)
+        if name == "bad_nan_tail":
+            x[174000:174100] = np.nan
+        elif name == "bad_inf_head":
+            x[0:10] = np.inf
+            x[10:20] = -np.inf
+        else:
+            x[:5000] = 0.0
+            x[160000:] = 0.0
+        kw = dict(bins_per_tone=2, steps_per_symbol=2, max_candidates=40, min_score=2, max_iterations=20)
+        with np.errstate(all="ignore"):
+            c = case(name, x, fs, kw, arrays, sub_rows=list(range(-20, 30)) + list(range(150, 176)))
+        c["payloads_sent"] = sent
+        out.append(c)
+    return out
+
+
 def main():
     scratch = tempfile.mkdtemp(prefix="ft8gold_")
     os.chdir(scratch)
-    if sys.argv[1:] == ["nochannel"]:
+    if sys.argv[1:] in (["nochannel"], ["nonfinite"]):
         with open(os.path.join(GOLD, "reftests.json")) as f:
             meta = json.load(f)
         old = np.load(os.path.join(GOLD, "reftests.npz"), allow_pickle=False)
         arrays = {k: old[k] for k in old.files}
-        new = nochannel_cases(arrays)
+        new = nochannel_cases(arrays) if sys.argv[1] == "nochannel" else nonfinite_cases(arrays)
         names = {c["name"] for c in new}
         meta["cases"] = [c for c in meta["cases"] if c["name"] not in names] + new
         np.savez_compressed(os.path.join(GOLD, "reftests.npz"), **arrays)
