@@ -132,3 +132,32 @@ def test_geometry_follows_the_float_sample_rate():
     for bad in (0, -1.0, float("nan"), float("inf")):
         with pytest.raises(ValueError):
             _lib.geometry(bad, 2, 2, 1000)
+
+
+@pytest.mark.gpu
+def test_gpu_batch_with_nonfinite_slots(reft, gpu):
+    """The bad_* slots and a clean one (ref_fs_frac is another rate, so a synthetic clean slot) in
+    ONE SlotDecoder batch: every slot's decodes equal its reference golden -- a NaN / inf slot
+    changes nothing in its neighbours (slot isolation through the compact score layout, the
+    selection, the LLR gathers and the persistent BP), in any order of the batch."""
+    import torch
+    from ft8_demodulator_amd import SlotDecoder, decode_ft8_message
+    cases, arr = reft
+    names = ["bad_nan_tail", "bad_inf_head", "bad_zero_half"]
+    clean = np.nan_to_num(arr["bad_nan_tail_x"], nan=0.0).astype(np.float32)
+    exp_clean = [(m.payload.hex(), t, f) for (m, _s, t, f, _sc) in
+                 decode_ft8_message(clean, 12000, **cases["bad_nan_tail"]["kwargs"])]
+    kw = cases[names[0]]["kwargs"]
+    dec = SlotDecoder(12000, kw["bins_per_tone"], kw["steps_per_symbol"], kw["max_candidates"], kw["min_score"],
+                      kw["max_iterations"])
+    for order in ([0, 1, 2, 3], [3, 2, 1, 0], [1, 3, 0, 2]):
+        xs = [arr[f"{n}_x"] for n in names] + [clean]
+        batch = torch.from_numpy(np.stack([xs[i] for i in order])).cuda()
+        got = dec.decode(batch)
+        for pos, i in enumerate(order):
+            g = [(m.payload.hex(), t, f) for (m, _s, t, f, _sc) in got[pos]]
+            if i < 3:
+                c = cases[names[i]]
+                assert g == [(r["payload"], r["time_sec"], r["freq_hz"]) for r in c["results"]], (order, names[i])
+            else:
+                assert g == exp_clean, order
