@@ -40,3 +40,33 @@ def test_reference_binding_matches_golden(golden, gpu):
         seen += 1
     assert seen >= 7
     assert rb.decode_ft8_message(np.zeros(1000, np.float32), 12000) == []
+
+
+def test_c_example_matches_golden(golden, gpu):
+    """examples/decode_wav.c: the C-ABI from plain C (WAV parsing, hipMalloc, ft8_decode_batch, the
+    reference's time / frequency arithmetic) reproduces the reference's golden decodes of every WAV
+    case it can express (the decode keywords without the band / time masks)."""
+    import subprocess
+    exe = os.path.join(ROOT, "examples", "decode_wav")
+    if not os.path.exists(exe):
+        pytest.fail("examples/decode_wav is not built (__graft_entry__.build() / make -C examples)")
+    meta, _ = golden
+    flag = {"max_candidates": "-k", "min_score": "-s", "max_iterations": "-i"}
+    seen = 0
+    for case in meta["e2e"]:
+        if "wav" not in case or case.get("as_float64") or case.get("as_analytic") or case["error"]:
+            continue
+        if set(case["kwargs"]) - set(flag):
+            continue
+        args = [exe, os.path.join(DATA, case["wav"])]
+        for k, v in case["kwargs"].items():
+            args += [flag[k], str(v)]
+        out = subprocess.run(args, capture_output=True, text=True, timeout=120, check=True).stdout.split("\n")
+        got = [ln.split() for ln in out if ln.strip()]
+        exp = case["results"]
+        assert [(g[0], int(g[1]), int(g[2]), int(g[3]), float(g[4]), float(g[5])) for g in got] == \
+               [(r["payload"], r["crc_calculated"], r["ldpc_errors"], r["crc_extracted"], r["time_sec"],
+                 r["freq_hz"]) for r in exp], case["name"]
+        assert np.allclose([float(g[6]) for g in got], [r["score"] for r in exp], rtol=0, atol=1e-4), case["name"]
+        seen += 1
+    assert seen >= 5
