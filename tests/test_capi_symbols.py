@@ -36,3 +36,27 @@ def test_host_entry_points_without_gpu():
     assert _lib.geometry(20000, 2, 2, 252800) == (3200, 1600, 6400, 157)
     assert _lib.geometry(12000, 2, 2, 1000)[3] == 0
     assert _lib.limits()["max_candidates"] == 4096
+
+
+def test_c_example_compiles_against_the_header(tmp_path):
+    """examples/decode_wav.c builds with gcc against include/ft8hip.h and links the in-tree
+    libft8hip.so (the header is plain C; ft8_params is the 64-byte ABI-2 block there too)."""
+    import shutil
+    import subprocess
+    gcc = shutil.which("gcc")
+    if gcc is None:
+        import pytest
+        pytest.skip("no gcc")
+    probe = tmp_path / "size.c"
+    probe.write_text('#include "ft8hip.h"\n#include <stddef.h>\n'
+                     '_Static_assert(sizeof(ft8_params) == 64, "ft8_params");\n'
+                     '_Static_assert(offsetof(ft8_params, sample_rate_hz) == 56, "sample_rate_hz");\n'
+                     '_Static_assert(sizeof(ft8_result) == 40, "ft8_result");\n'
+                     'int main(void) { return 0; }\n')
+    inc = os.path.join(ROOT, "include")
+    subprocess.run([gcc, "-std=c11", "-Wall", "-Werror", "-I", inc, "-o", str(tmp_path / "size"), str(probe)],
+                   check=True)
+    lib = os.path.join(ROOT, "ft8_demodulator_amd", "lib")
+    subprocess.run([gcc, "-O2", "-std=c11", "-Wall", "-Werror", "-I", inc, "-I", "/opt/rocm/include", "-o",
+                    str(tmp_path / "decode_wav"), os.path.join(ROOT, "examples", "decode_wav.c"), "-L", lib,
+                    "-lft8hip", "-L", "/opt/rocm/lib", "-lamdhip64"], check=True)
