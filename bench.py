@@ -738,7 +738,7 @@ def sensitivity(dev, rates=None, snr_lo=-24.0, snr_hi=-5.0, step=0.2, rounds=20,
     return {"method": "test_ft8_standard.py:43-123 on the GPU: f0 = fc = 0, bins_per_tone = steps_per_symbol = 2, "
                       "K = 20, min_score 1, 20 iterations, float64 input; SNR over the full band (B = fs / 2); "
                       f"{snr_lo} .. {snr_hi} dB in {step} dB steps (an extension of the reference's "
-                      "np.arange(-21, -10, 0.2) grid), {rounds} rounds per point; min_snr_db = the first point with "
+                      f"np.arange(-21, -10, 0.2) grid), {rounds} rounds per point; min_snr_db = the first point with "
                       ">= 50 % decodes on the wide grid; ref_rule_min_snr_db = the reference's rule on its own grid "
                       "(3 when no point of it reaches 50 %); crossing_50pct_db = the linear interpolation of the "
                       "success ratio at 0.5",
