@@ -107,7 +107,7 @@ def test_gpu_channel_fixture_drift_correction(gpu):
 
 
 def test_gpu_sensitivity_points_match_reference(gpu, oracle):
-    """The reference's own sensitivity harness (test_ft8_standard.py:43-123) at two of its rates,
+    """The reference's own sensitivity harness (test_ft8_standard.py:43-123) at seven of its rates,
     run here with the reference deciding success (tools/make_golden_sensitivity.py ->
     tests/golden/sensitivity_ref.json, 20 seeded rounds per SNR point): the GPU decodes the same
     float64 inputs and reaches the same verdict on every slot -- so the GPU sweep's thresholds

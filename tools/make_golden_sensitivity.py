@@ -1,4 +1,4 @@
-"""The reference's own sensitivity harness run here at two of its rates (build container only; imports
+"""The reference's own sensitivity harness run here at seven of its rates (build container only; imports
 /root/reference/src like tools/make_golden_harness.py): test_ft8_standard.py:43-68 test_step,
 `ROUNDS` rounds per SNR point, the reference's decode_ft8_message deciding success.  Inputs are
 seeded exactly as in make_golden_harness.py (np.random.default_rng(seed): payload, then noise; the
@@ -12,6 +12,7 @@ Usage:  cd /tmp && python /root/repo/tools/make_golden_sensitivity.py [extend]
         (extend: add only the rates not yet in tests/golden/sensitivity_ref.json)
 """
 import json
+import multiprocessing
 import os
 import sys
 import time
@@ -24,9 +25,20 @@ import make_golden_harness as MH  # noqa: E402  (reference import recipe, harnes
 POINTS = {2000: (-14.0, -13.0, -12.0, -11.0, -10.0), 6000: (-20.0, -19.0, -18.0, -17.0, -16.0, -15.0, -14.0),
           # round 6: a chirp-z rate (nfft 1760 = 2^5 * 5 * 11) and one >= 9 kHz, around the GPU table's
           # thresholds (-18.2 dB at 5 500 Hz, -20.6 dB at 10 000 Hz)
-          5500: (-19.5, -19.0, -18.5, -18.0, -17.5), 10000: (-21.5, -21.0, -20.5, -20.0, -19.5)}
+          5500: (-19.5, -19.0, -18.5, -18.0, -17.5), 10000: (-21.5, -21.0, -20.5, -20.0, -19.5),
+          # round 6, later: 3 000, 8 000 and 12 000 Hz around the 200-round GPU thresholds
+          # (-15.4, -19.6 and -21.4 dB, profiles/r6_y_sensitivity_200rounds.json)
+          3000: (-16.5, -16.0, -15.5, -15.0, -14.5), 8000: (-20.5, -20.0, -19.5, -19.0, -18.5),
+          12000: (-22.5, -22.0, -21.5, -21.0, -20.5)}
 ROUNDS = 20
 SEED0 = 70000
+
+
+def _verdict(job):
+    """One test_step of the harness: the reference's decode_ft8_message decides success."""
+    fs, snr, seed = job
+    _p, _c, x = MH.harness_input(fs, snr, seed)
+    return len(MH.quiet(MH.R.decode_ft8_message, x, fs, **MH.KW)) > 0
 
 
 def main():
@@ -47,13 +59,10 @@ def main():
             continue
         for snr in snrs:
             t0 = time.time()
-            seeds, ok = [], []
-            for _ in range(ROUNDS):
-                _p, _c, x = MH.harness_input(fs, snr, seed)
-                res = MH.quiet(MH.R.decode_ft8_message, x, fs, **MH.KW)
-                seeds.append(seed)
-                ok.append(len(res) > 0)
-                seed += 1
+            seeds = list(range(seed, seed + ROUNDS))
+            seed += ROUNDS
+            with multiprocessing.get_context("fork").Pool(min(8, os.cpu_count() or 1)) as pool:
+                ok = pool.map(_verdict, [(fs, snr, s_) for s_ in seeds])
             out["points"].append({"fs": fs, "snr_db": snr, "seeds": seeds, "success": ok,
                                   "ratio": sum(ok) / ROUNDS})
             print(fs, snr, sum(ok), "/", ROUNDS, round(time.time() - t0, 1), "s", flush=True)
